@@ -1,0 +1,401 @@
+// bc_capi.hip — extern "C" boundary (include/basecount_hip.h).  Host-side glue only: argument
+// checks, stream/memory management, launch geometry; every count/stat is computed by the
+// kernels in bc_kernels.hip.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "bc_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& m) {
+    g_err = m;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+    return fail(BC_E_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// Reads per kernel-1 workgroup: enough workgroups to fill 256 CUs several times over, and few
+// enough reads per chunk that a sorted chunk's positions fit one LDS window.
+int choose_rpb(int64_t n, int64_t L, int max_span, int sorted) {
+    if (const char* e = std::getenv("BC_RPB")) {
+        int v = std::atoi(e);
+        if (v > 0) return std::min(v, 32768);
+    }
+    int64_t target = std::min<int64_t>(8192, std::max<int64_t>(32, n / 2048));
+    if (!sorted || max_span <= 0 || max_span >= bc::kWinMax || L <= 0) return (int)target;
+    const double density = (double)n / (double)L;
+    const double fit = (bc::kWinMax - max_span) * density * 0.75;
+    if (fit >= 32.0) return (int)std::min<double>((double)target, fit);
+    return (int)target;  // sparse: chunks take the global-atomic path
+}
+
+bool host_sorted(const int32_t* pos, int64_t n) {
+    for (int64_t i = 1; i < n; ++i)
+        if (pos[i] < pos[i - 1]) return false;
+    return true;
+}
+
+int host_max_span(const bc_reads& r) {
+    uint64_t best = 0;
+    for (int64_t i = 0; i < r.n_reads; ++i) {
+        const uint32_t* cg = r.cigar + r.cig_beg[i];
+        uint64_t span = 0;
+        for (uint32_t k = 0; k < r.cig_n[i]; ++k) {
+            uint32_t op = cg[k] & 15u;
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) span += cg[k] >> 4;
+        }
+        best = std::max(best, span);
+    }
+    return (int)std::min<uint64_t>(best, 0x7fffffff);
+}
+
+int check_host_reads(const bc_reads* r) {
+    if (!r) return fail(BC_E_ARG, "reads is NULL");
+    if (r->n_reads < 0) return fail(BC_E_ARG, "n_reads < 0");
+    if (r->n_reads == 0) return BC_OK;
+    if (!r->pos || !r->cig_beg || !r->cig_n || !r->seq_nib) return fail(BC_E_ARG, "missing per-read array");
+    for (int64_t i = 0; i < r->n_reads; ++i) {
+        if ((uint64_t)r->cig_beg[i] + r->cig_n[i] > (uint64_t)r->n_cigar_words)
+            return fail(BC_E_ARG, "read " + std::to_string(i) + ": CIGAR outside the cigar buffer");
+        if (r->pos[i] < 0) return fail(BC_E_ARG, "read " + std::to_string(i) + ": negative start");
+        // query consumption must stay inside the packed sequence (and quality) buffers
+        uint64_t q = 0;
+        const uint32_t* cg = r->cigar + r->cig_beg[i];
+        for (uint32_t k = 0; k < r->cig_n[i]; ++k) {
+            uint32_t op = cg[k] & 15u;
+            if (op == 0 || op == 1 || op == 7 || op == 8) q += cg[k] >> 4;
+        }
+        if (q && (uint64_t)r->seq_nib[i] + q > 2ull * (uint64_t)r->seq_bytes)
+            return fail(BC_E_ARG, "read " + std::to_string(i) + ": CIGAR consumes past the sequence");
+        if (q && r->qual && (uint64_t)r->seq_nib[i] + q > (uint64_t)r->qual_bytes)
+            return fail(BC_E_ARG, "read " + std::to_string(i) + ": CIGAR consumes past the qualities");
+    }
+    return BC_OK;
+}
+
+// refPos the reference's .at() rejects first for read i (host walk in count.cpp:40-96 order)
+int64_t host_bad_pos(const bc_reads& r, int64_t i, int64_t ref_len, uint32_t mbq) {
+    static const int col_of[16] = {-1, 0, 1, -1, 2, -1, -1, -1, 3, -1, -1, -1, -1, -1, -1, 5};
+    int64_t rp = r.pos[i];
+    uint64_t qp = r.seq_nib[i];
+    const uint32_t* cg = r.cigar + r.cig_beg[i];
+    for (uint32_t k = 0; k < r.cig_n[i]; ++k) {
+        uint32_t op = cg[k] & 15u, len = cg[k] >> 4;
+        if (op == 0 || op == 7 || op == 8) {
+            for (uint32_t j = 0; j < len; ++j, ++rp, ++qp) {
+                if (r.qual && r.qual[qp] < mbq) continue;
+                if (!r.qual && mbq > 0) continue;
+                unsigned b = r.seq[qp >> 1];
+                unsigned nib = (qp & 1) ? (b & 15u) : (b >> 4);
+                if (col_of[nib] >= 0 && rp >= ref_len) return rp;
+            }
+        } else if (op == 1) {
+            qp += len;
+        } else if (op == 2 || op == 3) {
+            for (uint32_t j = 0; j < len; ++j, ++rp)
+                if (rp >= ref_len) return rp;
+        }
+    }
+    return -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* bc_last_error(void) { return g_err.c_str(); }
+int bc_abi_version(void) { return BC_ABI_VERSION; }
+
+int bc_device_count(int* n) {
+    if (!n) return fail(BC_E_ARG, "n is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = (e == hipSuccess) ? c : 0;
+    return BC_OK;
+}
+
+int bc_ctx_create(int device, void* stream, bc_ctx** out) {
+    if (!out) return fail(BC_E_ARG, "out is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(BC_E_NODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(BC_E_ARG, "device index out of range");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(BC_E_NODEV, std::string("built for gfx950, device is ") + prop.gcnArchName);
+    DeviceGuard g(device);
+    auto* c = new bc_ctx();
+    c->device = device;
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+    } else {
+        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete c;
+            return hip_fail(e, "hipStreamCreate");
+        }
+        c->own_stream = true;
+    }
+    hipError_t e = hipMalloc(&c->d_err, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipHostMalloc(&c->h_err, sizeof(unsigned long long), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_err, 0xFF, sizeof(unsigned long long), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        bc_ctx_destroy(c);
+        return hip_fail(e, "context scratch");
+    }
+    *out = c;
+    return BC_OK;
+}
+
+int bc_ctx_destroy(bc_ctx* c) {
+    if (!c) return BC_OK;
+    DeviceGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_err) (void)hipFree(c->d_err);
+    if (c->h_err) (void)hipHostFree(c->h_err);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return BC_OK;
+}
+
+int bc_ctx_stream(bc_ctx* c, void** s) {
+    if (!c || !s) return fail(BC_E_ARG, "NULL argument");
+    *s = (void*)c->stream;
+    return BC_OK;
+}
+
+int bc_sync(bc_ctx* c) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BC_OK;
+}
+
+int bc_malloc(bc_ctx* c, size_t bytes, void** p) {
+    if (!c || !p) return fail(BC_E_ARG, "NULL argument");
+    DeviceGuard g(c->device);
+    *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    HIP_TRY(hipMalloc(p, bytes));
+    return BC_OK;
+}
+
+int bc_free(bc_ctx* c, void* p) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (!p) return BC_OK;
+    DeviceGuard g(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(p));
+    return BC_OK;
+}
+
+int bc_memcpy_h2d(bc_ctx* c, void* d, const void* h, size_t bytes) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (!bytes) return BC_OK;
+    DeviceGuard g(c->device);
+    HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
+    return BC_OK;
+}
+
+int bc_memcpy_d2h(bc_ctx* c, void* h, const void* d, size_t bytes) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (!bytes) return BC_OK;
+    DeviceGuard g(c->device);
+    HIP_TRY(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
+    return BC_OK;
+}
+
+int bc_memset(bc_ctx* c, void* d, int v, size_t bytes) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (!bytes) return BC_OK;
+    DeviceGuard g(c->device);
+    HIP_TRY(hipMemsetAsync(d, v, bytes, c->stream));
+    return BC_OK;
+}
+
+int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
+    if (!c || !d) return fail(BC_E_ARG, "NULL argument");
+    int rc = check_host_reads(h);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    std::memset(d, 0, sizeof *d);
+    d->n_reads = h->n_reads;
+    d->n_cigar_words = h->n_cigar_words;
+    d->seq_bytes = h->seq_bytes;
+    d->qual_bytes = h->qual ? h->qual_bytes : 0;
+    d->sorted = h->n_reads ? (h->sorted ? 1 : (host_sorted(h->pos, h->n_reads) ? 1 : 0)) : 1;
+    d->max_span = h->max_span > 0 ? h->max_span : (h->n_reads ? host_max_span(*h) : 0);
+    const size_t n = (size_t)h->n_reads;
+    void* p[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const size_t sz[7] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4, (size_t)h->seq_bytes,
+                          h->qual ? (size_t)h->qual_bytes : 0};
+    const void* src[7] = {h->pos, h->cig_beg, h->cig_n, h->seq_nib, h->cigar, h->seq, h->qual};
+    for (int i = 0; i < 7; ++i) {
+        if (!sz[i]) continue;
+        hipError_t e = hipMalloc(&p[i], sz[i]);
+        if (e == hipSuccess) e = hipMemcpyAsync(p[i], src[i], sz[i], hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) {
+            for (int j = 0; j <= i; ++j)
+                if (p[j]) (void)hipFree(p[j]);
+            return hip_fail(e, "bc_reads_upload");
+        }
+    }
+    d->pos = (const int32_t*)p[0];
+    d->cig_beg = (const uint32_t*)p[1];
+    d->cig_n = (const uint32_t*)p[2];
+    d->seq_nib = (const uint32_t*)p[3];
+    d->cigar = (const uint32_t*)p[4];
+    d->seq = (const uint8_t*)p[5];
+    d->qual = (const uint8_t*)p[6];
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BC_OK;
+}
+
+int bc_reads_free(bc_ctx* c, bc_reads* d) {
+    if (!c || !d) return fail(BC_E_ARG, "NULL argument");
+    DeviceGuard g(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    const void* p[7] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual};
+    for (auto q : p)
+        if (q) (void)hipFree((void*)q);
+    std::memset(d, 0, sizeof *d);
+    return BC_OK;
+}
+
+int bc_count(bc_ctx* c, const bc_reads* r, int64_t ref_len, uint32_t mbq, int ncols, int32_t* d_hist) {
+    if (!c || !r) return fail(BC_E_ARG, "NULL argument");
+    if (ncols != 5 && ncols != 6) return fail(BC_E_ARG, "ncols must be 5 or 6");
+    if (ref_len < 0) return fail(BC_E_ARG, "ref_len < 0");
+    if (r->n_reads == 0) return BC_OK;
+    if (!d_hist && ref_len > 0) return fail(BC_E_ARG, "d_hist is NULL");
+    if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+    DeviceGuard g(c->device);
+    const int rpb = choose_rpb(r->n_reads, ref_len, r->max_span, r->sorted);
+    HIP_TRY(bc::launch_count(c->stream, *r, ref_len, mbq, ncols, d_hist, rpb, c->d_err));
+    return BC_OK;
+}
+
+int bc_range_error(bc_ctx* c, int64_t* first_bad) {
+    if (!c || !first_bad) return fail(BC_E_ARG, "NULL argument");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipMemcpyAsync(c->h_err, c->d_err, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_err, 0xFF, sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *first_bad = (*c->h_err == ~0ull) ? -1 : (int64_t)*c->h_err;
+    return BC_OK;
+}
+
+int bc_stats(bc_ctx* c, const int32_t* d_hist, int64_t L, int k, double nf, double nf2, int32_t* d_cov,
+             double* d_pc, double* d_ent, double* d_sec) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (k != 5 && k != 6) return fail(BC_E_ARG, "k must be 5 or 6");
+    if (L < 0) return fail(BC_E_ARG, "ref_len < 0");
+    if (L == 0) return BC_OK;
+    if (!d_hist) return fail(BC_E_ARG, "d_hist is NULL");
+    DeviceGuard g(c->device);
+    HIP_TRY(bc::launch_stats(c->stream, d_hist, L, k, nf, nf2, d_cov, d_pc, d_ent, d_sec));
+    return BC_OK;
+}
+
+size_t bc_summary_work_bytes(int64_t L) { return bc::summary_work_bytes(L); }
+
+int bc_summary(bc_ctx* c, const int32_t* d_cov, const double* d_ent, int64_t L, void* d_work, double* d_out) {
+    if (!c || !d_out || !d_work) return fail(BC_E_ARG, "NULL argument");
+    if (L <= 0) return fail(BC_E_ARG, "ref_len must be > 0 (np.mean of an empty list)");
+    if (!d_cov || !d_ent) return fail(BC_E_ARG, "NULL coverage / entropy");
+    DeviceGuard g(c->device);
+    HIP_TRY(bc::launch_summary(c->stream, d_cov, d_ent, L, d_work, d_out));
+    return BC_OK;
+}
+
+int bc_amplicons(bc_ctx* c, const int32_t* d_cov, const double* d_ent, const double* d_sec, int64_t L,
+                 const int64_t* d_lo, const int64_t* d_hi, int32_t n_tiles, double* d_out) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (n_tiles < 0) return fail(BC_E_ARG, "n_tiles < 0");
+    if (n_tiles == 0) return BC_OK;
+    if (!d_cov || !d_ent || !d_sec || !d_lo || !d_hi || !d_out) return fail(BC_E_ARG, "NULL argument");
+    DeviceGuard g(c->device);
+    HIP_TRY(bc::launch_amplicons(c->stream, d_cov, d_ent, d_sec, L, d_lo, d_hi, n_tiles, d_out));
+    return BC_OK;
+}
+
+int bc_bcount_host(int device, int64_t ref_len, uint32_t mbq, const bc_reads* h, uint32_t* h_out, int64_t* bad_read,
+                   int64_t* bad_pos) {
+    if (bad_read) *bad_read = -1;
+    if (bad_pos) *bad_pos = -1;
+    if (ref_len < 0 || ref_len > 0xFFFFFFFFll) return fail(BC_E_ARG, "refLen out of uint32 range");
+    if (ref_len > 0 && !h_out) return fail(BC_E_ARG, "h_out is NULL");
+    int rc = check_host_reads(h);
+    if (rc) return rc;
+    if (mbq > 0 && h->n_reads > 0 && !h->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+    bc_ctx* c = nullptr;
+    rc = bc_ctx_create(device, nullptr, &c);
+    if (rc) return rc;
+    struct Cleanup {
+        bc_ctx* c;
+        bc_reads d{};
+        int32_t* hist = nullptr;
+        ~Cleanup() {
+            if (hist) bc_free(c, hist);
+            bc_reads_free(c, &d);
+            bc_ctx_destroy(c);
+        }
+    } cl{c};
+    rc = bc_reads_upload(c, h, &cl.d);
+    if (rc) return rc;
+    const size_t hb = (size_t)std::max<int64_t>(ref_len, 1) * 6 * sizeof(int32_t);
+    rc = bc_malloc(c, hb, (void**)&cl.hist);
+    if (rc) return rc;
+    rc = bc_memset(c, cl.hist, 0, hb);
+    if (rc) return rc;
+    rc = bc_count(c, &cl.d, ref_len, mbq, 6, cl.hist);
+    if (rc) return rc;
+    int64_t bad = -1;
+    rc = bc_range_error(c, &bad);
+    if (rc) return rc;
+    if (bad >= 0) {
+        if (bad_read) *bad_read = bad;
+        const int64_t bp = host_bad_pos(*h, bad, ref_len, mbq);
+        if (bad_pos) *bad_pos = bp;
+        return fail(BC_E_RANGE, "vector::_M_range_check: __n (which is " + std::to_string(bp) +
+                                    ") >= this->size() (which is " + std::to_string(ref_len) + ")");
+    }
+    if (ref_len == 0) return BC_OK;
+    std::vector<int32_t> planes((size_t)ref_len * 6);
+    rc = bc_memcpy_d2h(c, planes.data(), cl.hist, (size_t)ref_len * 6 * sizeof(int32_t));
+    if (rc) return rc;
+    rc = bc_sync(c);
+    if (rc) return rc;
+    for (int64_t p = 0; p < ref_len; ++p)
+        for (int col = 0; col < 6; ++col) h_out[p * 6 + col] = (uint32_t)planes[(size_t)col * ref_len + p];
+    return BC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,40 @@
+// bc_internal.h — shared between the kernel file and the C-ABI file.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "basecount_hip.h"
+
+struct bc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    unsigned long long* d_err = nullptr;  // first out-of-range read index (atomicMin), ~0 = none
+    unsigned long long* h_err = nullptr;  // pinned mirror
+};
+
+namespace bc {
+
+// Kernel-1 geometry.  One 256-thread workgroup (4 waves) per chunk of consecutive reads.
+constexpr int kCountThreads = 256;
+// LDS window: counts of one chunk's reads, packed two 16-bit columns per 32-bit word
+// (planes {A|C, G|T, DS|N}); a chunk holds < 65536 reads so a 16-bit half never overflows.
+constexpr int kWinMax = 4096;  // positions per window -> 3 * 4096 * 4 B = 48 KiB
+constexpr int kStatsThreads = 256;
+constexpr int kNpBuf = 8192;   // numpy's default ufunc buffer size (reduction chunk)
+
+// launchers (bc_kernels.hip); all async on `s`, return hipError_t
+hipError_t launch_count(hipStream_t s, const bc_reads& r, int64_t ref_len, uint32_t mbq, int ncols,
+                        int32_t* hist, int reads_per_block, unsigned long long* d_err);
+hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span);
+hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2,
+                        int32_t* cov, double* pc, double* ent, double* sec);
+size_t summary_work_bytes(int64_t L);
+hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
+                          double* out);
+hipError_t launch_amplicons(hipStream_t s, const int32_t* cov, const double* ent, const double* sec,
+                            int64_t L, const int64_t* lo, const int64_t* hi, int n_tiles, double* out);
+
+}  // namespace bc

@@ -1,0 +1,606 @@
+// bc_kernels.hip — gfx950 kernels of the pileup counter.
+//
+//   k_count     kernel 1: CIGAR-expand + scatter-add (count.cpp:22-97)
+//   k_span      helper  : max reference span of a batch (sizes the LDS windows of kernel 1)
+//   k_stats     kernel 2: per-position coverage / percentages / entropies (main.py:14-79)
+//   k_sum_*     summary : numpy-exact mean of coverage and entropy (main.py:479-485)
+//   k_amplicon  amplicon: numpy-exact mean / median per tile window (main.py:519-551)
+//
+// Integer scatter, not a contraction: no MFMA.  Kernel 1 is bound by HBM (read records) and by
+// the LDS atomic rate; see DESIGN.md for the roofline accounting.
+#include "bc_internal.h"
+
+namespace bc {
+namespace {
+
+// BAM 4-bit code -> count column.  The reference switches on the ASCII letter of
+// query_alignment_sequence (count.cpp:58-65), which pysam decodes through "=ACMGRSVTWYHKDBN":
+// A(1)->0, C(2)->1, G(4)->2, T(8)->3, N(15)->5; every other code ('=' and IUPAC) counts nowhere.
+// Packed LUT, 4 bits per code, 0xF = not counted.
+constexpr unsigned long long kNibCol = 0x5FFFFFF3FFF2F10Full;
+__device__ __forceinline__ unsigned nib_col(unsigned nib) { return (unsigned)(kNibCol >> (nib * 4)) & 0xFu; }
+
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffff));
+    int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return ((int64_t)hi << 32) | (uint32_t)lo;
+}
+
+struct CountArgs {
+    const int32_t* pos;
+    const uint32_t* cig_beg;
+    const uint32_t* cig_n;
+    const uint32_t* seq_nib;
+    const uint32_t* cigar;
+    const uint8_t* seq;
+    const uint8_t* qual;
+    int64_t n;
+    int64_t ref_len;
+    uint32_t mbq;
+    int ncols;
+    int rpb;        // reads per workgroup chunk
+    int max_span;   // upper bound of any read's reference span
+    int sorted;
+    int32_t* hist;  // [ncols][ref_len]
+    unsigned long long* err;
+};
+
+// Walk one read with the whole wave (i is wave-uniform).  Lanes map to consecutive reference
+// events: event e of the read lies at reference position pos + e (M/=/X/D/N ops consume the
+// reference contiguously), so a 64-event window is 64 consecutive positions -> conflict-free
+// LDS addresses.  A scalar cursor (k, rc, qc) over the CIGAR skips ops that end before the
+// window; the per-window scan only touches ops overlapping it.
+template <bool QUAL, class Add>
+__device__ __forceinline__ bool walk_read(const CountArgs& A, int64_t i, unsigned lane, Add&& add) {
+    const int64_t p0 = A.pos[i];
+    const uint32_t* cg = A.cigar + A.cig_beg[i];
+    const uint32_t cn = A.cig_n[i];
+    const uint32_t sn = A.seq_nib[i];
+    bool bad = false;
+    uint32_t k = 0, rc = 0, qc = 0;  // op k starts at reference offset rc, query offset qc
+    for (uint32_t e0 = 0;; e0 += 64) {
+        // advance past ops that end at or before e0 (query-only ops on the way add to qc)
+        while (k < cn) {
+            const uint32_t w = cg[k], op = w & 15u, len = w >> 4;
+            const bool cref = (op == 0) | (op == 2) | (op == 3) | (op == 7) | (op == 8);
+            const bool cqry = (op == 0) | (op == 1) | (op == 7) | (op == 8);
+            if (cref && rc + len > e0) break;
+            rc += cref ? len : 0u;
+            qc += cqry ? len : 0u;
+            ++k;
+        }
+        if (k >= cn) break;
+        const uint32_t j = e0 + lane;
+        int typ = 0;  // 1 = aligned base, 2 = deletion / ref-skip
+        uint32_t qoff = 0;
+        uint32_t rcs = rc, qcs = qc;
+        for (uint32_t kk = k; kk < cn && rcs < e0 + 64u; ++kk) {
+            const uint32_t w = cg[kk], op = w & 15u, len = w >> 4;
+            const bool mref = (op == 0) | (op == 7) | (op == 8);
+            const bool dref = (op == 2) | (op == 3);
+            if (mref | dref) {
+                const uint32_t d = j - rcs;
+                if (d < len) {
+                    typ = mref ? 1 : 2;
+                    qoff = qcs + d;
+                }
+                rcs += len;
+            }
+            if (mref | (op == 1)) qcs += len;
+        }
+        if (typ) {
+            unsigned col = 4;  // DS: counted with no quality test (count.cpp:80-90)
+            bool counted = true;
+            if (typ == 1) {
+                const uint32_t ni = sn + qoff;
+                const unsigned byte = A.seq[ni >> 1];
+                col = nib_col((ni & 1u) ? (byte & 15u) : (byte >> 4));
+                counted = col != 0xFu;
+                if (QUAL) counted = counted && (uint32_t)A.qual[ni] >= A.mbq;  // count.cpp:56
+            }
+            if (counted) {
+                const int64_t rp = p0 + (int64_t)j;
+                if (rp >= A.ref_len || rp < 0)
+                    bad = true;  // .at() would throw (count.cpp:60-65,85)
+                else if ((int)col < A.ncols)
+                    add(col, rp);
+            }
+        }
+    }
+    return bad;
+}
+
+template <bool QUAL>
+__global__ __launch_bounds__(kCountThreads) void k_count(CountArgs A) {
+    __shared__ uint32_t win[3 * kWinMax];  // planes {A|C, G|T, DS|N}, 16-bit halves
+    const int64_t r0 = (int64_t)blockIdx.x * A.rpb;
+    const int64_t r1 = r0 + A.rpb < A.n ? r0 + A.rpb : A.n;
+    const unsigned lane = threadIdx.x & 63u;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int kWaves = kCountThreads / 64;
+
+    int64_t wbase = 0, wlen = 0;
+    bool use_lds = false;
+    if (A.sorted && A.max_span > 0) {
+        wbase = A.pos[r0];
+        wlen = (int64_t)A.pos[r1 - 1] - wbase + A.max_span;
+        use_lds = wlen <= kWinMax;
+    }
+    if (use_lds) {
+        for (int t = threadIdx.x; t < wlen; t += kCountThreads) {
+            win[t] = 0;
+            win[kWinMax + t] = 0;
+            win[2 * kWinMax + t] = 0;
+        }
+        __syncthreads();
+        for (int64_t i = r0 + wave; i < r1; i += kWaves) {
+            const int64_t iu = uni64(i);
+            bool bad = walk_read<QUAL>(A, iu, lane, [&](unsigned col, int64_t rp) {
+                const int64_t idx = rp - wbase;
+                if (idx >= 0 && idx < wlen)  // always true when pos is sorted and max_span holds
+                    atomicAdd(&win[(col >> 1) * kWinMax + (int)idx], 1u << ((col & 1u) * 16));
+                else
+                    atomicAdd(&A.hist[(int64_t)col * A.ref_len + rp], 1);
+            });
+            if (__any(bad) && lane == 0) atomicMin(A.err, (unsigned long long)iu);
+        }
+        __syncthreads();
+        // flush: one global atomic per nonzero (position, column) of the window
+        const int64_t L = A.ref_len;
+        for (int t = threadIdx.x; t < wlen; t += kCountThreads) {
+            const int64_t p = wbase + t;
+            if (p >= L) break;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const uint32_t v = win[pl * kWinMax + t];
+                const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
+                if (lo) atomicAdd(&A.hist[(int64_t)(2 * pl) * L + p], (int32_t)lo);
+                if (hi) atomicAdd(&A.hist[(int64_t)(2 * pl + 1) * L + p], (int32_t)hi);
+            }
+        }
+    } else {
+        // sparse / unsorted chunk: global atomics straight into the histogram
+        const int64_t L = A.ref_len;
+        for (int64_t i = r0 + wave; i < r1; i += kWaves) {
+            const int64_t iu = uni64(i);
+            bool bad = walk_read<QUAL>(A, iu, lane, [&](unsigned col, int64_t rp) {
+                atomicAdd(&A.hist[(int64_t)col * L + rp], 1);
+            });
+            if (__any(bad) && lane == 0) atomicMin(A.err, (unsigned long long)iu);
+        }
+    }
+}
+
+// max reference span over the batch (one thread per read)
+__global__ void k_span(const uint32_t* cig_beg, const uint32_t* cig_n, const uint32_t* cigar, int64_t n,
+                       int* out) {
+    int best = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t* cg = cigar + cig_beg[i];
+        uint32_t span = 0;
+        for (uint32_t k = 0, cn = cig_n[i]; k < cn; ++k) {
+            const uint32_t op = cg[k] & 15u;
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) span += cg[k] >> 4;
+        }
+        best = span > (uint32_t)best ? (int)span : best;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        int v = __shfl_down(best, o);
+        best = v > best ? v : best;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, best);
+}
+
+// ------------------------------------------------------------------------------ kernel 2
+// Same operation order as CPython evaluating main.py:37-53 (IEEE double, no contraction:
+// the file is compiled with -ffp-contract=off):
+//   probabilities = count / coverage; percentages = 100 * probability;
+//   entropy = nf * sum([-(x*log2(x)) if x != 0 else 0 ...])  (left to right from int 0)
+template <int K>
+__global__ __launch_bounds__(kStatsThreads) void k_stats(const int32_t* __restrict__ hist, int64_t L, double nf,
+                                                          double nf2, int32_t* __restrict__ cov_out,
+                                                          double* __restrict__ pc, double* __restrict__ ent,
+                                                          double* __restrict__ sec) {
+    for (int64_t p = (int64_t)blockIdx.x * kStatsThreads + threadIdx.x; p < L;
+         p += (int64_t)gridDim.x * kStatsThreads) {
+        int32_t c[K];
+        int64_t cov = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            c[j] = hist[(int64_t)j * L + p];
+            cov += c[j];
+        }
+        if (cov_out) cov_out[p] = (int32_t)cov;
+        if (cov == 0) {
+            if (pc) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) pc[(int64_t)j * L + p] = -1.0;
+            }
+            if (ent) ent[p] = 1.0;
+            if (sec) sec[p] = 1.0;
+            continue;
+        }
+        const double dcov = (double)cov;
+        double s = 0.0;
+        int am = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const double pj = (double)c[j] / dcov;
+            if (pc) pc[(int64_t)j * L + p] = 100.0 * pj;
+            if (c[j] != 0) s = s + (-(pj * log2(pj)));
+            if (c[j] > c[am]) am = j;  // np.argmax: first maximum
+        }
+        if (ent) ent[p] = nf * s;
+        if (sec) {
+            const int64_t cov2 = cov - c[am];
+            double h2 = 1.0;
+            if (cov2 != 0) {
+                const double d2 = (double)cov2;
+                double s2 = 0.0;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    if (j == am || c[j] == 0) continue;
+                    const double q = (double)c[j] / d2;
+                    s2 = s2 + (-(q * log2(q)));
+                }
+                h2 = nf2 * s2;
+            }
+            sec[p] = h2;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ numpy sums
+// numpy float64 add.reduce (numpy 2.2, verified against np.add.reduce / np.mean in
+// tests/test_npsum.py): the input is consumed in 8192-element buffers, s = 0; s += pw(buffer),
+// where pw is numpy's pairwise_sum: n < 8 -> sequential from 0.0; n <= 128 -> eight strided
+// accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail sequentially;
+// else split at n2 = n/2 - (n/2)%8 and add the halves.
+
+__device__ double pw_leaf(const double* a, int n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+}
+
+// Generic pairwise sum of a[0..m), m <= 8192, by one workgroup (any blockDim >= 128).
+// Thread 0 enumerates the leaves of numpy's recursion (<= 128 of them), the block sums the
+// leaves in parallel, thread 0 folds them back in the recursion's order.  Returns the value in
+// thread 0 only.
+__device__ double pw_block(const double* a, int m, int* s_off, int* s_len, double* s_val) {
+    __shared__ int s_nleaf;
+    if (threadIdx.x == 0) {
+        int stk_o[32], stk_l[32], sp = 0, nl = 0;
+        stk_o[sp] = 0;
+        stk_l[sp++] = m;
+        while (sp) {
+            const int o = stk_o[--sp], l = stk_l[sp];
+            if (l <= 128) {
+                s_off[nl] = o;
+                s_len[nl++] = l;
+            } else {
+                int n2 = l / 2;
+                n2 -= n2 % 8;
+                stk_o[sp] = o + n2;  // right first so left pops first
+                stk_l[sp++] = l - n2;
+                stk_o[sp] = o;
+                stk_l[sp++] = n2;
+            }
+        }
+        s_nleaf = nl;
+    }
+    __syncthreads();
+    const int nl = s_nleaf;
+    for (int t = threadIdx.x; t < nl; t += blockDim.x) s_val[t] = pw_leaf(a + s_off[t], s_len[t]);
+    __syncthreads();
+    double result = 0.0;
+    if (threadIdx.x == 0) {
+        // evaluate pw(m) recursively with an explicit stack; leaves consumed left to right
+        int st_len[32], st_stage[32];
+        double st_acc[32];
+        int sp = 0, leaf = 0;
+        st_len[0] = m;
+        st_stage[0] = 0;
+        sp = 1;
+        double ret = 0.0;
+        while (sp) {
+            const int top = sp - 1;
+            const int l = st_len[top];
+            if (l <= 128) {
+                ret = s_val[leaf++];
+                --sp;
+            } else {
+                int n2 = l / 2;
+                n2 -= n2 % 8;
+                if (st_stage[top] == 0) {
+                    st_stage[top] = 1;
+                    st_len[sp] = n2;
+                    st_stage[sp] = 0;
+                    ++sp;
+                    continue;
+                } else if (st_stage[top] == 1) {
+                    st_acc[top] = ret;
+                    st_stage[top] = 2;
+                    st_len[sp] = l - n2;
+                    st_stage[sp] = 0;
+                    ++sp;
+                    continue;
+                } else {
+                    ret = st_acc[top] + ret;
+                    --sp;
+                }
+            }
+        }
+        result = ret;
+    }
+    __syncthreads();
+    return result;
+}
+
+// Full 8192-element buffer with the fixed tree: 64 leaves of 128; 256 threads, thread t owns
+// accumulators {2(t&3), 2(t&3)+1} of leaf t>>2.  Value valid in thread 0.
+template <class F>
+__device__ double pw_full8192(F&& val, double* s_wave) {
+    const int t = threadIdx.x;
+    const int leaf = t >> 2, s = t & 3;
+    const int base = leaf * 128 + 2 * s;
+    double ra = val(base), rb = val(base + 1);
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+        ra += val(base + 8 * i);
+        rb += val(base + 8 * i + 1);
+    }
+    double v = ra + rb;              // (r0+r1), (r2+r3), (r4+r5), (r6+r7)
+    v = v + __shfl_down(v, 1);       // lanes s=0: (r0+r1)+(r2+r3); s=2: (r4+r5)+(r6+r7)
+    v = v + __shfl_down(v, 2);       // s=0: leaf value
+    v = v + __shfl_down(v, 4);       // pairs of leaves
+    v = v + __shfl_down(v, 8);
+    v = v + __shfl_down(v, 16);
+    v = v + __shfl_down(v, 32);      // lane 0: 16 leaves = pw(2048)
+    if ((t & 63) == 0) s_wave[t >> 6] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (t == 0) r = (s_wave[0] + s_wave[1]) + (s_wave[2] + s_wave[3]);
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ long long block_sum_i64(long long v, long long* s_red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    long long r = 0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r += s_red[w];
+    __syncthreads();
+    return r;
+}
+
+// one workgroup (256 threads) per 8192 buffer: entropy pairwise sum, exact coverage sum, nnz
+__global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const double* ent, int64_t L,
+                                                    double* part_ent, long long* part_cov, long long* part_nz) {
+    __shared__ double s_wave[4];
+    __shared__ long long s_red[4];
+    __shared__ int s_off[128], s_len[128];
+    __shared__ double s_val[128];
+    const int64_t c0 = (int64_t)blockIdx.x * kNpBuf;
+    const int m = (int)((L - c0) < kNpBuf ? (L - c0) : kNpBuf);
+    long long cs = 0, nz = 0;
+    for (int t = threadIdx.x; t < m; t += blockDim.x) {
+        const long long v = cov[c0 + t];
+        cs += v;
+        nz += v != 0;
+    }
+    cs = block_sum_i64(cs, s_red);
+    nz = block_sum_i64(nz, s_red);
+    double e;
+    if (m == kNpBuf)
+        e = pw_full8192([&](int i) { return ent[c0 + i]; }, s_wave);
+    else
+        e = pw_block(ent + c0, m, s_off, s_len, s_val);
+    if (threadIdx.x == 0) {
+        part_ent[blockIdx.x] = e;
+        part_cov[blockIdx.x] = cs;
+        part_nz[blockIdx.x] = nz;
+    }
+}
+
+__global__ void k_sum_final(const double* part_ent, const long long* part_cov, const long long* part_nz,
+                            int64_t nchunks, int64_t L, double* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double s = 0.0;
+    long long cs = 0, nz = 0;
+    for (int64_t c = 0; c < nchunks; ++c) {
+        s += part_ent[c];
+        cs += part_cov[c];
+        nz += part_nz[c];
+    }
+    const double n = (double)L;
+    out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
+    out[1] = s / n;
+    out[2] = (double)nz;
+    out[3] = (double)cs;
+}
+
+// ------------------------------------------------------------------------------ amplicons
+// k-th smallest (0-based) of n non-negative keys by 8-bit radix select (exact; np.median
+// takes the middle element(s) of the sorted values).
+template <class KeyF>
+__device__ unsigned long long radix_select(KeyF&& key, int64_t n, int64_t k, int bits, unsigned* s_hist,
+                                           unsigned long long* s_sel) {
+    unsigned long long prefix = 0, mask = 0;
+    for (int shift = bits - 8; shift >= 0; shift -= 8) {
+        for (int b = threadIdx.x; b < 256; b += blockDim.x) s_hist[b] = 0;
+        __syncthreads();
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const unsigned long long v = key(i);
+            if ((v & mask) == prefix) atomicAdd(&s_hist[(v >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t acc = 0;
+            int b = 0;
+            for (; b < 256; ++b) {
+                if (acc + s_hist[b] > k) break;
+                acc += s_hist[b];
+            }
+            s_sel[0] = (unsigned long long)b;
+            s_sel[1] = (unsigned long long)(k - acc);
+        }
+        __syncthreads();
+        prefix |= s_sel[0] << shift;
+        mask |= 255ull << shift;
+        k = (int64_t)s_sel[1];
+        __syncthreads();
+    }
+    return prefix;
+}
+
+__device__ double np_mean_block(const double* a, int64_t n, int* s_off, int* s_len, double* s_val) {
+    // s = 0; s += pw(buffer) per 8192 buffer; mean = s / n   (value valid in thread 0)
+    double s = 0.0;
+    for (int64_t c0 = 0; c0 < n; c0 += kNpBuf) {
+        const int m = (int)((n - c0) < kNpBuf ? (n - c0) : kNpBuf);
+        const double v = pw_block(a + c0, m, s_off, s_len, s_val);
+        s += v;
+    }
+    return s / (double)n;
+}
+
+__global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const double* ent, const double* sec, int64_t L,
+                                                  const int64_t* lo_a, const int64_t* hi_a, double* out) {
+    __shared__ unsigned s_hist[256];
+    __shared__ unsigned long long s_sel[2];
+    __shared__ long long s_red[4];
+    __shared__ int s_off[128], s_len[128];
+    __shared__ double s_val[128];
+    const int t = blockIdx.x;
+    int64_t lo = lo_a[t], hi = hi_a[t];
+    if (lo < 0) lo = 0;
+    if (hi > L - 1) hi = L - 1;
+    double* o = out + (int64_t)t * 6;
+    if (lo > hi) {
+        if (threadIdx.x == 0)
+            for (int j = 0; j < 6; ++j) o[j] = -1.0;
+        return;
+    }
+    const int64_t n = hi - lo + 1;
+    // coverage: exact integer mean, median via 32-bit select
+    long long cs = 0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) cs += cov[lo + i];
+    cs = block_sum_i64(cs, s_red);
+    const int64_t k1 = (n - 1) / 2, k2 = n / 2;
+    auto ckey = [&](int64_t i) { return (unsigned long long)(uint32_t)cov[lo + i]; };
+    const double c_a = (double)radix_select(ckey, n, k1, 32, s_hist, s_sel);
+    const double c_b = (k2 != k1) ? (double)radix_select(ckey, n, k2, 32, s_hist, s_sel) : c_a;
+    const double* vals[2] = {ent + lo, sec + lo};
+    double means[2], meds[2];
+    for (int q = 0; q < 2; ++q) {
+        const double* a = vals[q];
+        means[q] = np_mean_block(a, n, s_off, s_len, s_val);
+        auto dkey = [&](int64_t i) { return (unsigned long long)__double_as_longlong(a[i]); };
+        const double va = __longlong_as_double((long long)radix_select(dkey, n, k1, 64, s_hist, s_sel));
+        const double vb =
+            (k2 != k1) ? __longlong_as_double((long long)radix_select(dkey, n, k2, 64, s_hist, s_sel)) : va;
+        meds[q] = (k2 != k1) ? ((0.0 + va) + vb) / 2.0 : (0.0 + va) / 1.0;
+    }
+    if (threadIdx.x == 0) {
+        o[0] = (double)cs / (double)n;
+        o[1] = (k2 != k1) ? ((0.0 + c_a) + c_b) / 2.0 : c_a;
+        o[2] = means[0];
+        o[3] = meds[0];
+        o[4] = means[1];
+        o[5] = meds[1];
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ launchers
+hipError_t launch_count(hipStream_t s, const bc_reads& r, int64_t ref_len, uint32_t mbq, int ncols,
+                        int32_t* hist, int rpb, unsigned long long* d_err) {
+    if (r.n_reads <= 0) return hipSuccess;
+    CountArgs A;
+    A.pos = r.pos;
+    A.cig_beg = r.cig_beg;
+    A.cig_n = r.cig_n;
+    A.seq_nib = r.seq_nib;
+    A.cigar = r.cigar;
+    A.seq = r.seq;
+    A.qual = r.qual;
+    A.n = r.n_reads;
+    A.ref_len = ref_len;
+    A.mbq = mbq;
+    A.ncols = ncols;
+    A.rpb = rpb;
+    A.max_span = r.max_span;
+    A.sorted = r.sorted;
+    A.hist = hist;
+    A.err = d_err;
+    const int64_t nblk = (r.n_reads + rpb - 1) / rpb;
+    if (mbq > 0)
+        hipLaunchKernelGGL(k_count<true>, dim3((unsigned)nblk), dim3(kCountThreads), 0, s, A);
+    else
+        hipLaunchKernelGGL(k_count<false>, dim3((unsigned)nblk), dim3(kCountThreads), 0, s, A);
+    return hipGetLastError();
+}
+
+hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span) {
+    if (r.n_reads <= 0) return hipSuccess;
+    int64_t blocks = (r.n_reads + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_span, dim3((unsigned)blocks), dim3(256), 0, s, r.cig_beg, r.cig_n, r.cigar, r.n_reads,
+                       d_max_span);
+    return hipGetLastError();
+}
+
+hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2, int32_t* cov,
+                        double* pc, double* ent, double* sec) {
+    if (L <= 0) return hipSuccess;
+    int64_t blocks = (L + kStatsThreads - 1) / kStatsThreads;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    if (k == 5)
+        hipLaunchKernelGGL(k_stats<5>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, hist, L, nf, nf2, cov, pc,
+                           ent, sec);
+    else
+        hipLaunchKernelGGL(k_stats<6>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, hist, L, nf, nf2, cov, pc,
+                           ent, sec);
+    return hipGetLastError();
+}
+
+size_t summary_work_bytes(int64_t L) {
+    const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
+    return (size_t)(nc > 0 ? nc : 1) * 24;
+}
+
+hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work, double* out) {
+    const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
+    double* pe = (double*)work;
+    long long* pcv = (long long*)(pe + (nc > 0 ? nc : 1));
+    long long* pnz = pcv + (nc > 0 ? nc : 1);
+    if (nc > 0) hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)nc), dim3(256), 0, s, cov, ent, L, pe, pcv, pnz);
+    hipLaunchKernelGGL(k_sum_final, dim3(1), dim3(64), 0, s, pe, pcv, pnz, nc, L, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_amplicons(hipStream_t s, const int32_t* cov, const double* ent, const double* sec, int64_t L,
+                            const int64_t* lo, const int64_t* hi, int n_tiles, double* out) {
+    if (n_tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_amplicon, dim3((unsigned)n_tiles), dim3(256), 0, s, cov, ent, sec, L, lo, hi, out);
+    return hipGetLastError();
+}
+
+}  // namespace bc

@@ -1,0 +1,751 @@
+// bcio.cpp — host BAM decode / encode and byte-exact formatter (see include/bcio.h).
+//
+// Decode pipeline (replaces pysam at /root/reference/basecount/main.py:119-127):
+//   1. read the whole file, walk BGZF block headers (sequential, header hops only);
+//   2. inflate every block in parallel (raw deflate via zlib) into one contiguous buffer;
+//   3. parse the BAM header, hop over record lengths to find record starts (sequential);
+//   4. size pass + parallel fill of a struct-of-arrays that is uploaded to HBM as is.
+// The pysam fields the reference reads (main.py:165-173) are reproduced exactly:
+//   is_unmapped = flag & 4; mapping_quality; reference_start = pos; cigartuples (None if
+//   n_cigar == 0); query_alignment_sequence / _qualities = SEQ/QUAL[qstart:qend] where
+//   qstart/qend follow pysam's getQueryStart/getQueryEnd (leading S after optional H;
+//   trailing S walking back but never looking at op 0), None if l_seq == 0 or QUAL[0] == 0xFF.
+#include "../../include/bcio.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <charconv>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hw_threads(int n) {
+    if (n > 0) return n;
+    unsigned h = std::thread::hardware_concurrency();
+    return h ? (int)std::min(h, 16u) : 4;
+}
+
+template <class F>
+void parallel_for(int64_t n, int nthreads, F&& fn) {
+    // dynamic chunked loop; fn(begin, end)
+    if (n <= 0) return;
+    nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, n));
+    if (nthreads == 1) {
+        fn((int64_t)0, n);
+        return;
+    }
+    const int64_t chunk = std::max<int64_t>(1, n / (nthreads * 8));
+    std::atomic<int64_t> next{0};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < nthreads; ++t)
+        ts.emplace_back([&] {
+            for (;;) {
+                int64_t b = next.fetch_add(chunk);
+                if (b >= n) break;
+                fn(b, std::min(n, b + chunk));
+            }
+        });
+    for (auto& t : ts) t.join();
+}
+
+inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+inline uint32_t rd32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+inline int32_t rd32s(const uint8_t* p) { return (int32_t)rd32(p); }
+inline void wr16(std::string& s, uint16_t v) {
+    s.push_back((char)(v & 0xff));
+    s.push_back((char)(v >> 8));
+}
+inline void wr32(std::string& s, uint32_t v) {
+    for (int i = 0; i < 4; ++i) s.push_back((char)((v >> (8 * i)) & 0xff));
+}
+
+}  // namespace
+
+struct bcio_file {
+    std::vector<std::string> names;
+    std::vector<int64_t> lens;
+    // raw SoA
+    std::vector<int32_t> tid, pos, l_seq, qstart, qend;
+    std::vector<uint16_t> flag;
+    std::vector<uint8_t> mapq;
+    std::vector<uint32_t> rec_err;
+    std::vector<uint64_t> cig_off, seq_off;
+    std::vector<uint32_t> cigar;
+    std::vector<uint8_t> seq, qual;
+    // selection outputs
+    std::vector<int64_t> s_ref_beg, s_ordinal, s_rec;
+    std::vector<int32_t> s_pos;
+    std::vector<uint32_t> s_cig_beg, s_cig_n, s_seq_nib, s_qlen;
+};
+
+extern "C" const char* bcio_last_error(void) { return g_err.c_str(); }
+
+namespace {
+
+// pysam getQueryStart (libcalignedsegment.pyx): leading soft clips, hard clips allowed only at the
+// very start or once the whole query has been clipped.
+int32_t query_start(const uint32_t* cig, uint32_t n, int32_t l_qseq, bool* bad) {
+    int32_t start = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        uint32_t op = cig[k] & 0xf;
+        if (op == 5) {
+            if (start != 0 && start != l_qseq) *bad = true;
+        } else if (op == 4) {
+            start += (int32_t)(cig[k] >> 4);
+        } else {
+            break;
+        }
+    }
+    return start;
+}
+
+// pysam getQueryEnd: walk back from the last op, never looking at op 0.
+int32_t query_end(const uint32_t* cig, uint32_t n, int32_t l_qseq, bool* bad) {
+    int32_t end = l_qseq;
+    if (end == 0) {
+        for (uint32_t k = 0; k < n; ++k) {
+            uint32_t op = cig[k] & 0xf, len = cig[k] >> 4;
+            if (op == 0 || op == 1 || op == 7 || op == 8 || (op == 4 && end == 0)) end += (int32_t)len;
+        }
+    } else {
+        for (uint32_t k = n; k-- > 1;) {
+            uint32_t op = cig[k] & 0xf;
+            if (op == 5) {
+                if (end != l_qseq) *bad = true;
+            } else if (op == 4) {
+                end -= (int32_t)(cig[k] >> 4);
+            } else {
+                break;
+            }
+        }
+    }
+    return end;
+}
+
+struct Block {
+    uint64_t coff, clen, uoff;
+    uint32_t isize;
+};
+
+}  // namespace
+
+extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
+    if (!path || !out) return fail(BCIO_E_ARG, "null argument");
+    nthreads = hw_threads(nthreads);
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return fail(BCIO_E_IO, std::string("cannot open ") + path);
+    std::vector<uint8_t> comp;
+    {
+        std::fseek(fp, 0, SEEK_END);
+        long sz = std::ftell(fp);
+        std::fseek(fp, 0, SEEK_SET);
+        if (sz < 0) {
+            std::fclose(fp);
+            return fail(BCIO_E_IO, "ftell failed");
+        }
+        comp.resize((size_t)sz);
+        if (sz && std::fread(comp.data(), 1, (size_t)sz, fp) != (size_t)sz) {
+            std::fclose(fp);
+            return fail(BCIO_E_IO, "short read");
+        }
+        std::fclose(fp);
+    }
+    // 1. BGZF block scan
+    std::vector<Block> blocks;
+    uint64_t off = 0, uoff = 0;
+    while (off < comp.size()) {
+        if (comp.size() - off < 18) return fail(BCIO_E_FORMAT, "truncated BGZF header");
+        const uint8_t* h = comp.data() + off;
+        if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
+            return fail(BCIO_E_FORMAT, "not a BGZF file (bad gzip magic / no FEXTRA)");
+        uint16_t xlen = rd16(h + 10);
+        uint64_t bsize = 0;
+        bool found = false;
+        for (uint32_t x = 0; x + 4 <= xlen;) {
+            const uint8_t* sf = h + 12 + x;
+            uint16_t slen = rd16(sf + 2);
+            if (sf[0] == 66 && sf[1] == 67 && slen == 2) {
+                bsize = (uint64_t)rd16(sf + 4) + 1;
+                found = true;
+            }
+            x += 4 + slen;
+        }
+        if (!found) return fail(BCIO_E_FORMAT, "BGZF block without BC subfield");
+        if (off + bsize > comp.size()) return fail(BCIO_E_FORMAT, "truncated BGZF block");
+        Block b;
+        b.coff = off + 12 + xlen;
+        b.clen = bsize - xlen - 20;
+        b.isize = rd32(comp.data() + off + bsize - 4);
+        b.uoff = uoff;
+        uoff += b.isize;
+        blocks.push_back(b);
+        off += bsize;
+    }
+    // 2. parallel inflate
+    std::vector<uint8_t> raw(uoff);
+    std::atomic<int> zerr{0};
+    parallel_for((int64_t)blocks.size(), nthreads, [&](int64_t b0, int64_t b1) {
+        z_stream zs;
+        std::memset(&zs, 0, sizeof zs);
+        if (inflateInit2(&zs, -15) != Z_OK) {
+            zerr = 1;
+            return;
+        }
+        for (int64_t i = b0; i < b1; ++i) {
+            const Block& b = blocks[i];
+            if (b.isize == 0) continue;
+            inflateReset(&zs);
+            zs.next_in = comp.data() + b.coff;
+            zs.avail_in = (uInt)b.clen;
+            zs.next_out = raw.data() + b.uoff;
+            zs.avail_out = b.isize;
+            int r = inflate(&zs, Z_FINISH);
+            if (r != Z_STREAM_END || zs.avail_out != 0) zerr = 1;
+        }
+        inflateEnd(&zs);
+    });
+    if (zerr) return fail(BCIO_E_ZLIB, "inflate failed");
+    comp.clear();
+    comp.shrink_to_fit();
+
+    // 3. BAM header
+    auto* f = new bcio_file();
+    const uint8_t* p = raw.data();
+    const uint64_t N = raw.size();
+    auto bad = [&](const char* m) {
+        delete f;
+        return fail(BCIO_E_FORMAT, m);
+    };
+    if (N < 12 || std::memcmp(p, "BAM\1", 4) != 0) return bad("missing BAM magic");
+    uint64_t q = 4;
+    int32_t l_text = rd32s(p + q);
+    q += 4;
+    if (l_text < 0 || q + (uint64_t)l_text + 4 > N) return bad("bad header text length");
+    q += (uint64_t)l_text;
+    int32_t n_ref = rd32s(p + q);
+    q += 4;
+    if (n_ref < 0) return bad("negative n_ref");
+    for (int32_t i = 0; i < n_ref; ++i) {
+        if (q + 4 > N) return bad("truncated reference list");
+        int32_t ln = rd32s(p + q);
+        q += 4;
+        if (ln <= 0 || q + (uint64_t)ln + 4 > N) return bad("truncated reference name");
+        f->names.emplace_back((const char*)(p + q), strnlen((const char*)(p + q), (size_t)ln));
+        q += (uint64_t)ln;
+        f->lens.push_back((int64_t)rd32s(p + q));
+        q += 4;
+    }
+    // record starts
+    std::vector<uint64_t> starts;
+    while (q < N) {
+        if (q + 4 > N) return bad("truncated record length");
+        uint32_t bs = rd32(p + q);
+        if (bs < 32 || q + 4 + bs > N) return bad("truncated BAM record");
+        starts.push_back(q);
+        q += 4 + (uint64_t)bs;
+    }
+    const int64_t n = (int64_t)starts.size();
+    f->tid.resize(n);
+    f->pos.resize(n);
+    f->l_seq.resize(n);
+    f->qstart.resize(n);
+    f->qend.resize(n);
+    f->flag.resize(n);
+    f->mapq.resize(n);
+    f->rec_err.resize(n);
+    f->cig_off.resize(n + 1);
+    f->seq_off.resize(n + 1);
+    // 4a. size pass (sequential prefix sums of cigar / seq lengths)
+    f->cig_off[0] = 0;
+    f->seq_off[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* r = p + starts[i] + 4;
+        uint16_t nc = rd16(r + 12);
+        int32_t ls = rd32s(r + 16);
+        if (ls < 0) return bad("negative l_seq");
+        f->cig_off[i + 1] = f->cig_off[i] + nc;
+        f->seq_off[i + 1] = f->seq_off[i] + (uint64_t)((ls + 1) / 2);
+    }
+    f->cigar.resize(f->cig_off[n]);
+    f->seq.resize(f->seq_off[n]);
+    f->qual.assign(2 * f->seq_off[n], 0xFF);
+    std::atomic<int> ferr{0};
+    // 4b. parallel fill
+    parallel_for(n, nthreads, [&](int64_t b0, int64_t b1) {
+        for (int64_t i = b0; i < b1; ++i) {
+            const uint8_t* r = p + starts[i] + 4;
+            uint32_t bs = rd32(p + starts[i]);
+            int32_t t = rd32s(r + 0), ps = rd32s(r + 4);
+            uint8_t lrn = r[8], mq = r[9];
+            uint16_t nc = rd16(r + 12), fl = rd16(r + 14);
+            int32_t ls = rd32s(r + 16);
+            uint64_t need = 32 + (uint64_t)lrn + 4ull * nc + (uint64_t)((ls + 1) / 2) + (uint64_t)ls;
+            if (need > bs) {
+                ferr = 1;
+                continue;
+            }
+            f->tid[i] = t;
+            f->pos[i] = ps;
+            f->mapq[i] = mq;
+            f->flag[i] = fl;
+            f->l_seq[i] = ls;
+            const uint8_t* c = r + 32 + lrn;
+            uint32_t* cd = f->cigar.data() + f->cig_off[i];
+            for (uint16_t k = 0; k < nc; ++k) cd[k] = rd32(c + 4 * k);
+            const uint8_t* s = c + 4ull * nc;
+            uint64_t sb = (uint64_t)((ls + 1) / 2);
+            std::memcpy(f->seq.data() + f->seq_off[i], s, sb);
+            const uint8_t* ql = s + sb;
+            std::memcpy(f->qual.data() + 2 * f->seq_off[i], ql, (size_t)ls);
+            uint32_t err = 0;
+            if (nc == 0) err |= BCIO_REC_NO_CIGAR;
+            if (ls == 0) err |= BCIO_REC_NO_SEQ;
+            if (ls == 0 || ql[0] == 0xFF) err |= BCIO_REC_NO_QUAL;
+            bool badclip = false;
+            f->qstart[i] = query_start(cd, nc, ls, &badclip);
+            f->qend[i] = query_end(cd, nc, ls, &badclip);
+            if (badclip) err |= BCIO_REC_BAD_CLIP;
+            if (ps < 0) err |= BCIO_REC_NEG_POS;
+            f->rec_err[i] = err;
+        }
+    });
+    if (ferr) return bad("BAM record shorter than its fields");
+    *out = f;
+    return BCIO_OK;
+}
+
+extern "C" void bcio_close(bcio_file* f) { delete f; }
+extern "C" int32_t bcio_n_refs(const bcio_file* f) { return f ? (int32_t)f->names.size() : 0; }
+extern "C" const char* bcio_ref_name(const bcio_file* f, int32_t i) {
+    return (f && i >= 0 && i < (int32_t)f->names.size()) ? f->names[i].c_str() : nullptr;
+}
+extern "C" int64_t bcio_ref_len(const bcio_file* f, int32_t i) {
+    return (f && i >= 0 && i < (int32_t)f->lens.size()) ? f->lens[i] : -1;
+}
+
+extern "C" int bcio_get_records(const bcio_file* f, bcio_records* o) {
+    if (!f || !o) return fail(BCIO_E_ARG, "null argument");
+    o->n = (int64_t)f->tid.size();
+    o->tid = f->tid.data();
+    o->pos = f->pos.data();
+    o->flag = f->flag.data();
+    o->mapq = f->mapq.data();
+    o->l_seq = f->l_seq.data();
+    o->qstart = f->qstart.data();
+    o->qend = f->qend.data();
+    o->rec_err = f->rec_err.data();
+    o->cig_off = f->cig_off.data();
+    o->cigar = f->cigar.data();
+    o->seq_off = f->seq_off.data();
+    o->seq = f->seq.data();
+    o->qual = f->qual.data();
+    o->seq_bytes = f->seq_off.empty() ? 0 : f->seq_off.back();
+    return BCIO_OK;
+}
+
+extern "C" int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_sel, bcio_selection* o) {
+    if (!f || !o || !ref_sel) return fail(BCIO_E_ARG, "null argument");
+    const int64_t n = (int64_t)f->tid.size();
+    const int32_t nr = (int32_t)f->names.size();
+    std::vector<int64_t> cnt(nr + 1, 0);
+    int64_t ordinal = 0;
+    o->keyerror_ordinal = -1;
+    o->keyerror_rec = -1;
+    // accepted = mapped and mapq >= mmq (main.py:165); is_unmapped is flag bit 4 only.
+    for (int64_t i = 0; i < n; ++i) {
+        if ((f->flag[i] & 4) || (int64_t)f->mapq[i] < min_mapq) continue;
+        int32_t t = f->tid[i];
+        if (t < 0 || t >= nr || !ref_sel[t]) {
+            if (o->keyerror_ordinal < 0) {
+                o->keyerror_ordinal = ordinal;
+                o->keyerror_rec = i;
+            }
+        } else {
+            cnt[t + 1]++;
+        }
+        ordinal++;
+    }
+    o->n_accepted = ordinal;
+    f->s_ref_beg.assign(nr + 1, 0);
+    for (int32_t t = 0; t < nr; ++t) f->s_ref_beg[t + 1] = f->s_ref_beg[t] + cnt[t + 1];
+    const int64_t m = f->s_ref_beg[nr];
+    f->s_pos.resize(m);
+    f->s_cig_beg.resize(m);
+    f->s_cig_n.resize(m);
+    f->s_seq_nib.resize(m);
+    f->s_qlen.resize(m);
+    f->s_ordinal.resize(m);
+    f->s_rec.resize(m);
+    std::vector<int64_t> fill(f->s_ref_beg.begin(), f->s_ref_beg.end() - 1);
+    ordinal = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if ((f->flag[i] & 4) || (int64_t)f->mapq[i] < min_mapq) continue;
+        int32_t t = f->tid[i];
+        if (t >= 0 && t < nr && ref_sel[t]) {
+            int64_t j = fill[t]++;
+            f->s_pos[j] = f->pos[i];
+            f->s_cig_beg[j] = (uint32_t)f->cig_off[i];
+            f->s_cig_n[j] = (uint32_t)(f->cig_off[i + 1] - f->cig_off[i]);
+            f->s_seq_nib[j] = (uint32_t)(2 * f->seq_off[i] + (uint64_t)std::max(0, f->qstart[i]));
+            int32_t ql = f->qend[i] - f->qstart[i];
+            f->s_qlen[j] = (uint32_t)std::max(0, ql);
+            f->s_ordinal[j] = ordinal;
+            f->s_rec[j] = i;
+        }
+        ordinal++;
+    }
+    o->ref_beg = f->s_ref_beg.data();
+    o->pos = f->s_pos.data();
+    o->cig_beg = f->s_cig_beg.data();
+    o->cig_n = f->s_cig_n.data();
+    o->seq_nib = f->s_seq_nib.data();
+    o->qlen = f->s_qlen.data();
+    o->ordinal = f->s_ordinal.data();
+    o->rec = f->s_rec.data();
+    if (f->cig_off.back() > 0xFFFFFFFFull || 2 * f->seq_off.back() > 0xFFFFFFFFull)
+        return fail(BCIO_E_ARG, "file too large for 32-bit batch offsets; split it");
+    return BCIO_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// writer
+namespace {
+
+// htslib reg2bin (SAM spec §5.3), end exclusive
+int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+const uint8_t kEOF[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+}  // namespace
+
+extern "C" int bcio_write_bam(const char* path, const bcio_write_spec* s) {
+    if (!path || !s) return fail(BCIO_E_ARG, "null argument");
+    // serialize uncompressed stream
+    std::string u;
+    u.append("BAM\1", 4);
+    std::string text = "@HD\tVN:1.6\tSO:unknown\n";
+    for (int32_t i = 0; i < s->n_refs; ++i)
+        text += std::string("@SQ\tSN:") + s->ref_names[i] + "\tLN:" + std::to_string(s->ref_lens[i]) + "\n";
+    wr32(u, (uint32_t)text.size());
+    u += text;
+    wr32(u, (uint32_t)s->n_refs);
+    for (int32_t i = 0; i < s->n_refs; ++i) {
+        std::string nm = s->ref_names[i];
+        wr32(u, (uint32_t)(nm.size() + 1));
+        u += nm;
+        u.push_back('\0');
+        wr32(u, (uint32_t)s->ref_lens[i]);
+    }
+    for (int64_t i = 0; i < s->n; ++i) {
+        char name[32];
+        int ln = std::snprintf(name, sizeof name, "r%lld", (long long)i) + 1;
+        uint32_t nc = (uint32_t)(s->cig_off[i + 1] - s->cig_off[i]);
+        int32_t ls = s->l_seq[i];
+        uint64_t sb = (uint64_t)((ls + 1) / 2);
+        uint32_t bs = (uint32_t)(32 + ln + 4 * nc + sb + (uint64_t)ls);
+        const uint32_t* cg = s->cigar + s->cig_off[i];
+        int64_t span = 0;
+        for (uint32_t k = 0; k < nc; ++k) {
+            uint32_t op = cg[k] & 0xf;
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) span += cg[k] >> 4;
+        }
+        int64_t beg = s->pos[i] < 0 ? 0 : s->pos[i];
+        int bin = reg2bin(beg, beg + (span > 0 ? span : 1));
+        wr32(u, bs);
+        wr32(u, (uint32_t)s->tid[i]);
+        wr32(u, (uint32_t)s->pos[i]);
+        u.push_back((char)ln);
+        u.push_back((char)s->mapq[i]);
+        wr16(u, (uint16_t)bin);
+        wr16(u, (uint16_t)nc);
+        wr16(u, s->flag[i]);
+        wr32(u, (uint32_t)ls);
+        wr32(u, 0xFFFFFFFFu);
+        wr32(u, 0xFFFFFFFFu);
+        wr32(u, 0);
+        u.append(name, (size_t)ln);
+        for (uint32_t k = 0; k < nc; ++k) wr32(u, cg[k]);
+        u.append((const char*)(s->seq + s->seq_off[i]), sb);
+        if (s->qual_off[i + 1] - s->qual_off[i] == (uint64_t)ls)
+            u.append((const char*)(s->qual + s->qual_off[i]), (size_t)ls);
+        else
+            u.append((size_t)ls, (char)0xFF);
+    }
+    // BGZF compress in 64 KiB - 256 B input blocks, in parallel
+    const size_t kIn = 65280;
+    const size_t nb = (u.size() + kIn - 1) / kIn;
+    std::vector<std::string> outb(nb);
+    std::atomic<int> zerr{0};
+    parallel_for((int64_t)nb, hw_threads(s->nthreads), [&](int64_t b0, int64_t b1) {
+        for (int64_t b = b0; b < b1; ++b) {
+            const uint8_t* src = (const uint8_t*)u.data() + b * kIn;
+            size_t len = std::min(kIn, u.size() - b * kIn);
+            z_stream zs;
+            std::memset(&zs, 0, sizeof zs);
+            if (deflateInit2(&zs, s->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+                zerr = 1;
+                return;
+            }
+            std::vector<uint8_t> cbuf(deflateBound(&zs, (uLong)len) + 64);
+            zs.next_in = (Bytef*)src;
+            zs.avail_in = (uInt)len;
+            zs.next_out = cbuf.data();
+            zs.avail_out = (uInt)cbuf.size();
+            if (deflate(&zs, Z_FINISH) != Z_STREAM_END) zerr = 1;
+            size_t clen = zs.total_out;
+            deflateEnd(&zs);
+            if (clen + 26 > 65536) {  // incompressible: store
+                clen = 0;
+                zerr = 2;
+            }
+            uint32_t crc = (uint32_t)crc32(0L, src, (uInt)len);
+            std::string& o = outb[b];
+            const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 0, 0};
+            o.assign((const char*)hdr, 18);
+            uint16_t bsize = (uint16_t)(clen + 25);
+            o[16] = (char)(bsize & 0xff);
+            o[17] = (char)(bsize >> 8);
+            o.append((const char*)cbuf.data(), clen);
+            wr32(o, crc);
+            wr32(o, (uint32_t)len);
+        }
+    });
+    if (zerr) return fail(BCIO_E_ZLIB, "deflate failed (block does not fit BGZF)");
+    FILE* fp = std::fopen(path, "wb");
+    if (!fp) return fail(BCIO_E_IO, std::string("cannot create ") + path);
+    for (auto& o : outb) std::fwrite(o.data(), 1, o.size(), fp);
+    std::fwrite(kEOF, 1, sizeof kEOF, fp);
+    if (std::fclose(fp) != 0) return fail(BCIO_E_IO, "write failed");
+    return BCIO_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// formatter: str(round(x, dp)) exactly as CPython 3.10 (Objects/floatobject.c double_round +
+// Python/pystrtod.c format_float_short 'r').  round(): correctly rounded decimal with dp digits
+// (half-even on the exact binary value) parsed back to the nearest double; glibc printf and
+// strtod are both exact, so printf("%.*f") + strtod is the same map.  repr(): shortest digits
+// that round-trip (std::to_chars), fixed notation for 1e-4 <= |y| < 1e16, else d.ddde+XX.
+namespace {
+
+int py_repr(double y, char* out) {
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof buf, y, std::chars_format::scientific);
+    *r.ptr = 0;
+    // parse [-]d[.ddd]e[+-]xx
+    const char* s = buf;
+    char* o = out;
+    if (*s == '-') {
+        *o++ = '-';
+        ++s;
+    }
+    char digits[40];
+    int nd = 0;
+    while (*s && *s != 'e') {
+        if (*s != '.') digits[nd++] = *s;
+        ++s;
+    }
+    int e10 = 0;
+    if (*s == 'e') e10 = std::atoi(s + 1);
+    // strip trailing zeros (to_chars shortest never emits them except for "0")
+    while (nd > 1 && digits[nd - 1] == '0') --nd;
+    int decpt = e10 + 1;
+    if (nd == 1 && digits[0] == '0') decpt = 1;  // zero
+    if (decpt <= -4 || decpt > 16) {
+        *o++ = digits[0];
+        if (nd > 1) {
+            *o++ = '.';
+            for (int i = 1; i < nd; ++i) *o++ = digits[i];
+        }
+        o += std::sprintf(o, "e%+.02d", decpt - 1);
+    } else if (decpt <= 0) {
+        *o++ = '0';
+        *o++ = '.';
+        for (int i = 0; i < -decpt; ++i) *o++ = '0';
+        for (int i = 0; i < nd; ++i) *o++ = digits[i];
+    } else if (decpt >= nd) {
+        for (int i = 0; i < nd; ++i) *o++ = digits[i];
+        for (int i = nd; i < decpt; ++i) *o++ = '0';
+        *o++ = '.';
+        *o++ = '0';
+    } else {
+        for (int i = 0; i < decpt; ++i) *o++ = digits[i];
+        *o++ = '.';
+        for (int i = decpt; i < nd; ++i) *o++ = digits[i];
+    }
+    *o = 0;
+    return (int)(o - out);
+}
+
+inline int py_round_float(double x, int dp, char* out) {
+    double y = x;
+    if (std::isfinite(x) && dp <= 323) {
+        char b[400];
+        std::snprintf(b, sizeof b, "%.*f", dp, x);
+        y = std::strtod(b, nullptr);
+    }
+    return py_repr(y, out);
+}
+
+inline int py_int(int64_t v, char* out) {
+    auto r = std::to_chars(out, out + 24, v);
+    *r.ptr = 0;
+    return (int)(r.ptr - out);
+}
+
+}  // namespace
+
+struct bcio_fmt {
+    std::string buf;
+    bool taken = false;
+};
+
+extern "C" int bcio_fmt_new(bcio_fmt** out) {
+    if (!out) return fail(BCIO_E_ARG, "null");
+    *out = new bcio_fmt();
+    return BCIO_OK;
+}
+extern "C" void bcio_fmt_free(bcio_fmt* b) { delete b; }
+extern "C" int bcio_fmt_take(bcio_fmt* b, const char** data, int64_t* size) {
+    if (!b) return fail(BCIO_E_ARG, "null");
+    *data = b->buf.data();
+    *size = (int64_t)b->buf.size();
+    b->taken = true;
+    return BCIO_OK;
+}
+extern "C" int bcio_fmt_pyround_float(double x, int dp, char* out, int cap) {
+    if (cap < 400 || dp < 0 || dp > 323) return fail(BCIO_E_ARG, "bad dp/cap");
+    return py_round_float(x, dp, out);
+}
+extern "C" int bcio_fmt_pyround_int(int64_t v, int dp, char* out, int cap) {
+    if (cap < 24 || dp < 0) return fail(BCIO_E_ARG, "bad dp/cap");
+    return py_int(v, out);
+}
+
+extern "C" int bcio_fmt_rows(bcio_fmt* b, const char* ref, int64_t L, int k, const int32_t* counts,
+                             const double* pc, const double* ent, const double* sec, int dp,
+                             int long_format, int nthreads) {
+    if (!b || !ref || (k != 5 && k != 6) || dp < 0 || dp > 323 || L < 0)
+        return fail(BCIO_E_ARG, "bad formatter arguments");
+    if (b->taken) {
+        b->buf.clear();
+        b->taken = false;
+    }
+    static const char* kBase[6] = {"A", "C", "G", "T", "DS", "N"};
+    const std::string refs(ref);
+    nthreads = hw_threads(nthreads);
+    const int64_t per = 1 << 14;
+    const int64_t nchunks = (L + per - 1) / per;
+    std::vector<std::string> parts((size_t)nchunks);
+    parallel_for(nchunks, nthreads, [&](int64_t c0, int64_t c1) {
+        char tmp[512];
+        for (int64_t c = c0; c < c1; ++c) {
+            std::string& s = parts[(size_t)c];
+            const int64_t p0 = c * per, p1 = std::min(L, p0 + per);
+            s.reserve((size_t)(p1 - p0) * (long_format ? 6 * 48 : 96));
+            for (int64_t p = p0; p < p1; ++p) {
+                int64_t cov = 0;
+                int nz = 0;
+                for (int j = 0; j < k; ++j) {
+                    cov += counts[(int64_t)j * L + p];
+                    nz += counts[(int64_t)j * L + p] != 0;
+                }
+                // entropy / secondary text, shared by all k long rows
+                char et[400], st[400];
+                if (cov == 0) {
+                    std::strcpy(et, "1");
+                    std::strcpy(st, "1");
+                } else {
+                    py_round_float(ent[p], dp, et);
+                    if (nz <= 1)
+                        std::strcpy(st, "1");
+                    else
+                        py_round_float(sec[p], dp, st);
+                }
+                char post[24], covt[24];
+                py_int(p + 1, post);
+                py_int(cov, covt);
+                if (!long_format) {
+                    s += refs;
+                    s += '\t';
+                    s += post;
+                    s += '\t';
+                    s += covt;
+                    for (int j = 0; j < k; ++j) {
+                        s += '\t';
+                        py_int(counts[(int64_t)j * L + p], tmp);
+                        s += tmp;
+                    }
+                    for (int j = 0; j < k; ++j) {
+                        s += '\t';
+                        if (cov == 0)
+                            s += "-1";
+                        else {
+                            py_round_float(pc[(int64_t)j * L + p], dp, tmp);
+                            s += tmp;
+                        }
+                    }
+                    s += '\t';
+                    s += et;
+                    s += '\t';
+                    s += st;
+                    s += '\n';
+                } else {
+                    for (int j = 0; j < k; ++j) {
+                        s += refs;
+                        s += '\t';
+                        s += post;
+                        s += '\t';
+                        s += covt;
+                        s += '\t';
+                        s += kBase[j];
+                        s += '\t';
+                        py_int(counts[(int64_t)j * L + p], tmp);
+                        s += tmp;
+                        s += '\t';
+                        if (cov == 0)
+                            s += "-1";
+                        else {
+                            py_round_float(pc[(int64_t)j * L + p], dp, tmp);
+                            s += tmp;
+                        }
+                        s += '\t';
+                        s += et;
+                        s += '\t';
+                        s += st;
+                        s += '\n';
+                    }
+                }
+            }
+        }
+    });
+    size_t tot = b->buf.size();
+    for (auto& s : parts) tot += s.size();
+    b->buf.reserve(tot);
+    for (auto& s : parts) b->buf += s;
+    return BCIO_OK;
+}

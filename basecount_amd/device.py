@@ -1,0 +1,230 @@
+"""ctypes bindings for ``libbasecount_hip.so`` (``include/basecount_hip.h``).
+
+``Context`` wraps one ``bc_ctx`` (device + stream); ``DeviceBuffer`` is a library-owned HBM
+allocation; ``DeviceReads`` is an uploaded read batch (``bc_reads``).  Pointers may also come
+from another allocator (e.g. ``torch.Tensor.data_ptr()``) — the C-ABI only sees addresses.
+
+There is no CPU fallback: if the library or a gfx950 device is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._native import _libs, _load
+
+BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV = -1, -2, -3, -4
+
+
+class BcReads(C.Structure):
+    _fields_ = [
+        ("n_reads", C.c_int64),
+        ("pos", C.c_void_p),
+        ("cig_beg", C.c_void_p),
+        ("cig_n", C.c_void_p),
+        ("seq_nib", C.c_void_p),
+        ("cigar", C.c_void_p),
+        ("n_cigar_words", C.c_int64),
+        ("seq", C.c_void_p),
+        ("seq_bytes", C.c_int64),
+        ("qual", C.c_void_p),
+        ("qual_bytes", C.c_int64),
+        ("sorted", C.c_int32),
+        ("max_span", C.c_int32),
+    ]
+
+
+class BcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    L = _libs.get("libbasecount_hip.so")
+    if L is not None:
+        return L
+    L = _load("libbasecount_hip.so")
+    vp, i64, u32, dbl = C.c_void_p, C.c_int64, C.c_uint32, C.c_double
+    sig = {
+        "bc_last_error": ([], C.c_char_p),
+        "bc_abi_version": ([], C.c_int),
+        "bc_device_count": ([C.POINTER(C.c_int)], C.c_int),
+        "bc_ctx_create": ([C.c_int, vp, C.POINTER(vp)], C.c_int),
+        "bc_ctx_destroy": ([vp], C.c_int),
+        "bc_ctx_stream": ([vp, C.POINTER(vp)], C.c_int),
+        "bc_sync": ([vp], C.c_int),
+        "bc_malloc": ([vp, C.c_size_t, C.POINTER(vp)], C.c_int),
+        "bc_free": ([vp, vp], C.c_int),
+        "bc_memcpy_h2d": ([vp, vp, vp, C.c_size_t], C.c_int),
+        "bc_memcpy_d2h": ([vp, vp, vp, C.c_size_t], C.c_int),
+        "bc_memset": ([vp, vp, C.c_int, C.c_size_t], C.c_int),
+        "bc_reads_upload": ([vp, C.POINTER(BcReads), C.POINTER(BcReads)], C.c_int),
+        "bc_reads_free": ([vp, C.POINTER(BcReads)], C.c_int),
+        "bc_count": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, vp], C.c_int),
+        "bc_range_error": ([vp, C.POINTER(i64)], C.c_int),
+        "bc_stats": ([vp, vp, i64, C.c_int, dbl, dbl, vp, vp, vp, vp], C.c_int),
+        "bc_summary_work_bytes": ([i64], C.c_size_t),
+        "bc_summary": ([vp, vp, vp, i64, vp, vp], C.c_int),
+        "bc_amplicons": ([vp, vp, vp, vp, i64, vp, vp, C.c_int32, vp], C.c_int),
+        "bc_bcount_host": ([C.c_int, i64, u32, C.POINTER(BcReads), vp, C.POINTER(i64),
+                            C.POINTER(i64)], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise BcError(rc, lib().bc_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().bc_device_count(C.byref(n)))
+    return n.value
+
+
+class DeviceBuffer:
+    """Library-owned HBM allocation."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(lib().bc_malloc(ctx.h, self.nbytes, C.byref(p)))
+        self.ptr = p.value
+
+    def free(self):
+        if self.ptr:
+            check(lib().bc_free(self.ctx.h, self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def upload(self, arr: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        check(lib().bc_memcpy_h2d(self.ctx.h, self.ptr, a.ctypes.data, a.nbytes))
+        self.ctx._keep.append(a)  # keep host staging alive until the next sync
+        return self
+
+    def download(self, dtype, count: int, offset_bytes: int = 0) -> np.ndarray:
+        out = np.empty(int(count), dtype)
+        if out.nbytes:
+            check(lib().bc_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr + offset_bytes,
+                                      out.nbytes))
+            self.ctx.sync()
+        return out
+
+    def zero(self, nbytes: int | None = None):
+        check(lib().bc_memset(self.ctx.h, self.ptr, 0, self.nbytes if nbytes is None else nbytes))
+
+
+def host_reads(b: dict) -> tuple:
+    """bc_reads over host numpy arrays (keeps the arrays referenced in the returned tuple)."""
+    keep = {}
+    for k, dt in (("pos", np.int32), ("cig_beg", np.uint32), ("cig_n", np.uint32),
+                  ("seq_nib", np.uint32), ("cigar", np.uint32), ("seq", np.uint8)):
+        keep[k] = np.ascontiguousarray(b[k], dt)
+    q = b.get("qual")
+    keep["qual"] = None if q is None else np.ascontiguousarray(q, np.uint8)
+    r = BcReads()
+    r.n_reads = keep["pos"].size
+    for k in ("pos", "cig_beg", "cig_n", "seq_nib", "cigar", "seq"):
+        setattr(r, k, keep[k].ctypes.data if keep[k].size else None)
+    r.n_cigar_words = keep["cigar"].size
+    r.seq_bytes = keep["seq"].size
+    if keep["qual"] is not None:
+        r.qual = keep["qual"].ctypes.data if keep["qual"].size else None
+        r.qual_bytes = keep["qual"].size
+    r.sorted = int(b.get("sorted", 0))
+    r.max_span = int(b.get("max_span", 0))
+    return r, keep
+
+
+class DeviceReads:
+    """A read batch resident in HBM (library-owned copy of a host batch)."""
+
+    def __init__(self, ctx: "Context", b: dict):
+        self.ctx = ctx
+        hr, keep = host_reads(b)
+        self.r = BcReads()
+        check(lib().bc_reads_upload(ctx.h, C.byref(hr), C.byref(self.r)))
+        self.n = int(self.r.n_reads)
+
+    def free(self):
+        if getattr(self, "r", None) is not None and self.ctx.h:
+            check(lib().bc_reads_free(self.ctx.h, C.byref(self.r)))
+            self.r = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    def __init__(self, device: int = 0, stream: int | None = None):
+        self.device = int(device)
+        h = C.c_void_p()
+        check(lib().bc_ctx_create(self.device, stream, C.byref(h)))
+        self.h = h.value
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            lib().bc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(lib().bc_sync(self.h))
+        self._keep.clear()
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        check(lib().bc_ctx_stream(self.h, C.byref(s)))
+        return s.value or 0
+
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    # kernels ---------------------------------------------------------------------------
+    def count(self, reads, ref_len: int, mbq: int, ncols: int, d_hist: int) -> None:
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        check(lib().bc_count(self.h, C.byref(r), int(ref_len), int(mbq), int(ncols), d_hist))
+
+    def range_error(self) -> int:
+        v = C.c_int64(-1)
+        check(lib().bc_range_error(self.h, C.byref(v)))
+        return v.value
+
+    def stats(self, d_hist, L, k, nf, nf2, d_cov, d_pc, d_ent, d_sec) -> None:
+        check(lib().bc_stats(self.h, d_hist, int(L), int(k), float(nf), float(nf2), d_cov, d_pc,
+                             d_ent, d_sec))
+
+    def summary(self, d_cov, d_ent, L, d_work, d_out) -> None:
+        check(lib().bc_summary(self.h, d_cov, d_ent, int(L), d_work, d_out))
+
+    def amplicons(self, d_cov, d_ent, d_sec, L, d_lo, d_hi, n_tiles, d_out) -> None:
+        check(lib().bc_amplicons(self.h, d_cov, d_ent, d_sec, int(L), d_lo, d_hi, int(n_tiles),
+                                 d_out))
+
+
+def summary_work_bytes(L: int) -> int:
+    return int(lib().bc_summary_work_bytes(int(L)))

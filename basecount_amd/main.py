@@ -1,0 +1,662 @@
+"""Host orchestration: the reference's Python layer (/root/reference/basecount/main.py) driving the
+MI355X kernels.
+
+Same public surface as the reference — ``get_entropy``, ``get_stats``, ``get_references``,
+``open_samfile``, ``init_read_chunk``, ``get_basecounts``, ``BaseCount`` (``rows``, ``records``,
+``num_reads``, ``mean_coverage``, ``mean_entropy``, ``columns``, ``references``,
+``reference_lengths``, ``data``), ``handle_arg`` and the ``run`` CLI — with the same outputs,
+argument meanings and exceptions.  What changes is where the work happens:
+
+  reference                                   here
+  pysam read loop (main.py:127-174)           native BAM decoder + numpy filter (bam.py)
+  count.bcount per chunk (main.py:146,179)    kernel 1 on the whole reference at once (HBM)
+  np.add of chunks (main.py:155,188)          device-resident int32 histogram
+  get_stats Python loop (main.py:29-78)       kernel 2 (fp64, same operation order)
+  summary / amplicon loops (main.py:469-551)  numpy-exact device reductions (bc_summary /
+                                              bc_amplicons)
+
+Chunking (``chunk_size``) cannot change counts (integer sums commute); it only decides WHICH
+error the reference raises first when the input has several faults, so the same timeline is
+replayed from the fault positions (``_first_error``).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import math
+import os
+from array import array
+
+import numpy as np
+
+from . import device as D
+from . import fmt
+from .bam import REC_BAD_CLIP, REC_NEG_POS, REC_NO_CIGAR, REC_NO_QUAL, REC_NO_SEQ, BamFile
+from .scheme import load_scheme
+from .version import __version__
+
+_TYPE_FAULTS = REC_NO_CIGAR | REC_NO_SEQ | REC_NO_QUAL | REC_NEG_POS
+_SIG = (
+    "bcount(): incompatible function arguments. The following argument types are supported:\n"
+    "    1. (arg0: typing.SupportsInt | typing.SupportsIndex, arg1: typing.SupportsInt | "
+    "typing.SupportsIndex, arg2: collections.abc.Sequence[str], arg3: collections.abc.Sequence"
+    "[collections.abc.Sequence[typing.SupportsInt | typing.SupportsIndex]], arg4: collections."
+    "abc.Sequence[typing.SupportsInt | typing.SupportsIndex], arg5: collections.abc.Sequence"
+    "[collections.abc.Sequence[tuple[typing.SupportsInt | typing.SupportsIndex, typing."
+    "SupportsInt | typing.SupportsIndex]]]) -> list[list[int]]\n\nInvoked with: "
+)
+_U32 = 1 << 32
+_CONTEXTS: dict = {}
+
+
+def default_device() -> int:
+    for var in ("BASECOUNT_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v not in (None, ""):
+            return int(v)
+    return 0
+
+
+def context(device: int | None = None) -> D.Context:
+    dev = default_device() if device is None else int(device)
+    ctx = _CONTEXTS.get(dev)
+    if ctx is None:
+        ctx = _CONTEXTS[dev] = D.Context(dev)
+    return ctx
+
+
+def norm_factors(k: int):
+    """main.py:24-25: 1/log2(k), 1/log2(k-1) evaluated exactly as the reference does."""
+    return 1 / math.log2(k), 1 / math.log2(k - 1)
+
+
+# ------------------------------------------------------------------------- API parity helpers
+def get_entropy(probabilities):
+    """main.py:10-11."""
+    return sum([-(x * math.log2(x)) if x != 0 else 0 for x in probabilities])
+
+
+class RefData:
+    """Per-position results of one reference, host-resident (downloaded from HBM).
+
+    counts: int32 [k][L]; pc: f64 [k][L]; ent, sec: f64 [L]; cov: int32 [L]."""
+
+    __slots__ = ("counts", "pc", "ent", "sec", "cov")
+
+    def __init__(self, counts, pc, ent, sec, cov):
+        self.counts, self.pc, self.ent, self.sec, self.cov = counts, pc, ent, sec, cov
+
+    @property
+    def L(self) -> int:
+        return int(self.cov.size)
+
+
+class Rows:
+    """Sequence of the reference's row lists (main.py:57-78), built lazily from a RefData with
+    the reference's Python types (ints where it has ints)."""
+
+    def __init__(self, ref: str, d: RefData, long_format: bool):
+        self.ref, self.d, self.long = ref, d, long_format
+        self.k = d.counts.shape[0]
+
+    def __len__(self):
+        return self.d.L * (self.k if self.long else 1)
+
+    def _position(self, p, cnt, pcs, e, s):
+        cov = sum(cnt)
+        if cov == 0:
+            return cov, cnt, [-1] * self.k, 1, 1
+        nz = sum(1 for v in cnt if v)
+        return cov, cnt, pcs, e, (1 if nz <= 1 else s)
+
+    def __iter__(self):
+        d, k, ref = self.d, self.k, self.ref
+        cols = [c.tolist() for c in d.counts]
+        pcs = [c.tolist() for c in d.pc]
+        ent, sec = d.ent.tolist(), d.sec.tolist()
+        bases = fmt.BASES[:k]
+        for p in range(d.L):
+            cov, cnt, pc, e, s = self._position(p, [c[p] for c in cols], [c[p] for c in pcs],
+                                                ent[p], sec[p])
+            if self.long:
+                for j in range(k):
+                    yield [ref, p + 1, cov, bases[j], cnt[j], pc[j], e, s]
+            else:
+                yield [ref, p + 1, cov] + cnt + pc + [e, s]
+
+    def __getitem__(self, i):
+        n = len(self)
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(n))]
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError("list index out of range")
+        p, j = (divmod(i, self.k) if self.long else (i, None))
+        d = self.d
+        cov, cnt, pc, e, s = self._position(
+            p, [int(v) for v in d.counts[:, p]], [float(v) for v in d.pc[:, p]], float(d.ent[p]),
+            float(d.sec[p]))
+        if self.long:
+            return [self.ref, p + 1, cov, fmt.BASES[j], cnt[j], pc[j], e, s]
+        return [self.ref, p + 1, cov] + cnt + pc + [e, s]
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+
+def get_stats(base_counts, ref, show_n_bases=False, long_format=False):
+    """main.py:14-79 on the device (kernel 2).  ``base_counts``: refLen x 6 counts."""
+    a = np.asarray(base_counts, dtype=np.int64).reshape(-1, 6)
+    if not show_n_bases and isinstance(base_counts, list):
+        for bc in base_counts:  # the reference pops N from the caller's lists (main.py:31)
+            if isinstance(bc, list):
+                bc.pop(5)
+    k = 6 if show_n_bases else 5
+    d = stats_on_device(np.ascontiguousarray(a[:, :k].T.astype(np.int32)), k)
+    return list(Rows(ref, d, long_format))
+
+
+def stats_on_device(planes: np.ndarray, k: int, device: int | None = None) -> RefData:
+    """Kernel 2 over host count planes int32 [k][L] (used by get_stats / the bcount adapter)."""
+    ctx = context(device)
+    L = planes.shape[1]
+    if L == 0:
+        return RefData(planes, np.zeros((k, 0)), np.zeros(0), np.zeros(0), np.zeros(0, np.int32))
+    hist = ctx.alloc(planes.nbytes).upload(planes)
+    outs = _alloc_outputs(ctx, k, L, want_pc=True)
+    nf, nf2 = norm_factors(k)
+    ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, outs["pc"].ptr, outs["ent"].ptr,
+              outs["sec"].ptr)
+    return _download(outs, planes.copy(), k, L)
+
+
+def _alloc_outputs(ctx, k, L, want_pc):
+    o = {"cov": ctx.alloc(4 * L), "ent": ctx.alloc(8 * L), "sec": ctx.alloc(8 * L)}
+    o["pc"] = ctx.alloc(8 * k * L) if want_pc else None
+    return o
+
+
+def _download(outs, counts, k, L) -> RefData:
+    cov = outs["cov"].download(np.int32, L)
+    ent = outs["ent"].download(np.float64, L)
+    sec = outs["sec"].download(np.float64, L)
+    pc = outs["pc"].download(np.float64, k * L).reshape(k, L)
+    return RefData(counts, pc, ent, sec, cov)
+
+
+def get_references(samfile, references=None):
+    """main.py:82-92 (returns a set: its iteration order is the output order)."""
+    if references is None:
+        references = samfile.references
+    else:
+        for reference in references:
+            if not (reference in samfile.references):
+                raise Exception(f"{reference} is not a valid reference")
+    return set(references)
+
+
+def open_samfile(bam):
+    """main.py:95-100 (no htslib messages to silence: the decoder is ours)."""
+    return BamFile(bam)
+
+
+def init_read_chunk(references):
+    """main.py:103-107 (kept for API parity; the device path does not chunk)."""
+    return {ref: {"reads": [], "qualities": [], "starts": [], "ctuples": []} for ref in references}
+
+
+# ------------------------------------------------------------------------- error timeline
+def _pysam_args(f: BamFile, recs):
+    reads, quals, starts, ctuples = [], [], [], []
+    for r in recs:
+        r = int(r)
+        reads.append(f.query_alignment_sequence(r))
+        q = f.query_alignment_qualities(r)
+        quals.append(None if q is None else array("B", q.tobytes()))
+        starts.append(int(f.pos[r]))
+        ctuples.append(f.cigartuples(r))
+    return reads, quals, starts, ctuples
+
+
+def _bad_pos(f: BamFile, rec: int, mbq: int, L: int) -> int:
+    """refPos that the reference's .at() rejects first for record ``rec`` (count.cpp:40-96)."""
+    rp = int(f.pos[rec])
+    qp = 2 * int(f.seq_off[rec]) + int(f.qstart[rec])
+    a, b = int(f.cig_off[rec]), int(f.cig_off[rec + 1])
+    for w in f.cigar[a:b].tolist():
+        op, ln = w & 15, w >> 4
+        if op in (0, 7, 8):
+            for _ in range(ln):
+                if int(f.qual[qp]) >= mbq:
+                    byte = int(f.seq[qp >> 1])
+                    nib = byte & 15 if qp & 1 else byte >> 4
+                    if nib in (1, 2, 4, 8, 15) and rp >= L:
+                        return rp
+                rp += 1
+                qp += 1
+        elif op == 1:
+            qp += ln
+        elif op in (2, 3):
+            for _ in range(ln):
+                if rp >= L:
+                    return rp
+                rp += 1
+    return -1
+
+
+def _first_error(f, sel, ref_order, ref_index, lengths, mbq, cs, type_ord, range_idx):
+    """Replay the reference's read loop / chunk-flush timeline (main.py:141-189) and return the
+    exception it raises first, or None.
+
+    type_ord[ref]  : first accepted-read ordinal of the ref with a None field / negative start
+    range_idx[ref] : first batch index whose counted event lies outside the reference
+    """
+    mbq_bad = not (0 <= mbq < _U32)
+    # in-loop faults: KeyError for an unrequested reference (main.py:166), pysam's ValueError
+    # for invalid clipping when a selected read's sequence is fetched (main.py:167)
+    inloop = None
+    if sel.keyerror_ordinal >= 0:
+        t = int(f.tid[sel.keyerror_rec])
+        name = f.references[t] if 0 <= t < len(f.references) else None
+        inloop = (sel.keyerror_ordinal, KeyError(name))
+    clip = (f.rec_err[sel.rec] & REC_BAD_CLIP) != 0
+    if clip.any():
+        o = int(sel.ordinal[np.argmax(clip)])
+        if inloop is None or o < inloop[0]:
+            inloop = (o, ValueError("Invalid clipping in CIGAR string"))
+
+    def chunk_of(o):
+        return o // cs if cs > 0 else 0
+
+    faults = {}  # ref -> (chunk, kind, ordinal/idx)
+    for ref in ref_order:
+        cand = []
+        if mbq_bad:
+            cand.append((0, 0, "type", None))
+        if type_ord.get(ref, -1) >= 0:
+            cand.append((chunk_of(type_ord[ref]), 0, "type", None))
+        if range_idx.get(ref, -1) >= 0:
+            t = ref_index[ref]
+            o = int(sel.ordinal[sel.ref_beg[t] + range_idx[ref]])
+            cand.append((chunk_of(o), 1, "range", range_idx[ref]))
+        if cand:
+            faults[ref] = min(cand, key=lambda c: (c[0], c[1]))
+    if cs == 0 and mbq_bad and f.n_records > 0 and ref_order:
+        inloop = None  # the empty flush at the first record raises before anything else
+    if not faults:
+        return inloop[1] if inloop else None
+    kf = min(v[0] for v in faults.values())
+    if inloop is not None:
+        if cs <= 0 or kf >= inloop[0] // cs:
+            return inloop[1]
+    for ref in ref_order:
+        v = faults.get(ref)
+        if v is None or v[0] != kf:
+            continue
+        t = ref_index[ref]
+        b0, b1 = int(sel.ref_beg[t]), int(sel.ref_beg[t + 1])
+        if v[2] == "type":
+            ords = sel.ordinal[b0:b1]
+            m = (ords // cs == kf) if cs > 0 else np.ones(b1 - b0, bool)
+            recs = sel.rec[b0:b1][m]
+            args = [lengths[ref], mbq] + list(_pysam_args(f, recs))
+            return TypeError(_SIG + ", ".join(repr(a) for a in args))
+        rec = int(sel.rec[b0 + v[3]])
+        L = lengths[ref]
+        return IndexError(f"vector::_M_range_check: __n (which is {_bad_pos(f, rec, mbq, L)}) "
+                          f">= this->size() (which is {L})")
+    return None
+
+
+# ------------------------------------------------------------------------- device pipeline
+class _FileOnDevice:
+    """Shared per-file buffers in HBM: CIGAR words, packed SEQ, nibble-indexed QUAL, and the
+    per-read arrays of every selected read (sliced per reference)."""
+
+    def __init__(self, ctx: D.Context, f: BamFile, sel, need_qual: bool):
+        self.ctx = ctx
+        rec_err = f.rec_err[sel.rec] if sel.rec.size else np.zeros(0, np.uint32)
+        faulty = (rec_err & (_TYPE_FAULTS | REC_BAD_CLIP)) != 0
+        # faulty reads raise before their counts could matter: give them no CIGAR so the range
+        # check only ever reports well-formed reads
+        self.cig_n = np.where(faulty, 0, sel.cig_n).astype(np.uint32)
+        self.pos = np.where(faulty, 0, sel.pos).astype(np.int32)
+        self.sel = sel
+        # reference spans per record (for the LDS window bound)
+        op = f.cigar & 0xF
+        ln = (f.cigar >> 4).astype(np.int64)
+        cons = (op == 0) | (op == 2) | (op == 3) | (op == 7) | (op == 8)
+        csum = np.zeros(f.cigar.size + 1, np.int64)
+        np.cumsum(np.where(cons, ln, 0), out=csum[1:])
+        span = csum[f.cig_off[1:].astype(np.int64)] - csum[f.cig_off[:-1].astype(np.int64)]
+        self.span = np.where(faulty, 0, span[sel.rec]) if sel.rec.size else np.zeros(0, np.int64)
+        self.d_cigar = ctx.alloc(max(4, f.cigar.nbytes)).upload(f.cigar)
+        self.d_seq = ctx.alloc(max(4, f.seq.nbytes)).upload(f.seq)
+        self.d_qual = ctx.alloc(max(4, f.qual.nbytes)).upload(f.qual) if need_qual else None
+        self.n_cig, self.n_seq, self.n_qual = f.cigar.size, f.seq.size, f.qual.size
+        m = sel.pos.size
+        self.d_pos = ctx.alloc(max(4, 4 * m)).upload(self.pos)
+        self.d_cb = ctx.alloc(max(4, 4 * m)).upload(sel.cig_beg)
+        self.d_cn = ctx.alloc(max(4, 4 * m)).upload(self.cig_n)
+        self.d_sn = ctx.alloc(max(4, 4 * m)).upload(sel.seq_nib)
+
+    def reads(self, t: int) -> D.BcReads:
+        b0, b1 = int(self.sel.ref_beg[t]), int(self.sel.ref_beg[t + 1])
+        r = D.BcReads()
+        r.n_reads = b1 - b0
+        r.pos = self.d_pos.ptr + 4 * b0
+        r.cig_beg = self.d_cb.ptr + 4 * b0
+        r.cig_n = self.d_cn.ptr + 4 * b0
+        r.seq_nib = self.d_sn.ptr + 4 * b0
+        r.cigar = self.d_cigar.ptr
+        r.n_cigar_words = self.n_cig
+        r.seq = self.d_seq.ptr
+        r.seq_bytes = self.n_seq
+        if self.d_qual is not None:
+            r.qual = self.d_qual.ptr
+            r.qual_bytes = self.n_qual
+        pos = self.pos[b0:b1]
+        r.sorted = int(bool(np.all(pos[1:] >= pos[:-1]))) if b1 - b0 > 1 else 1
+        r.max_span = int(min(self.span[b0:b1].max(), 2**31 - 1)) if b1 > b0 else 0
+        return r
+
+
+def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality=0,
+                   chunk_size=1000000, show_n_bases=False, long_format=False, *, device=None,
+                   _mode="rows", _tiles=None):
+    """main.py:110-205 on the device.  Returns {ref: {"rows": Rows, "num_reads": n}} in the
+    reference's (set) order.  ``_mode="summary"`` keeps per-position data in HBM and returns
+    the numpy-exact summary (and amplicon) reductions instead of rows."""
+    samfile = open_samfile(bam)
+    try:
+        references = get_references(samfile, references)
+        names = samfile.references
+        ref_index = {n: i for i, n in enumerate(names)}
+        reference_lengths = {ref: samfile.lengths[names.index(ref)] for ref in references}
+        ref_order = list(references)
+        sel = samfile.select(min_mapping_quality, [n in references for n in names])
+        mbq = int(min_base_quality)
+        k = 6 if show_n_bases else 5
+        ncols = k  # N is only ever reported with show_n_bases
+        rec_err = samfile.rec_err[sel.rec] if sel.rec.size else np.zeros(0, np.uint32)
+        type_ord = {}
+        for ref in ref_order:
+            t = ref_index[ref]
+            b0, b1 = int(sel.ref_beg[t]), int(sel.ref_beg[t + 1])
+            m = (rec_err[b0:b1] & _TYPE_FAULTS) != 0
+            type_ord[ref] = int(sel.ordinal[b0 + int(np.argmax(m))]) if m.any() else -1
+
+        results, range_idx = {}, {}
+        if 0 <= mbq < _U32:
+            ctx = context(device)
+            fod = _FileOnDevice(ctx, samfile, sel, need_qual=mbq > 0)
+            nf, nf2 = norm_factors(k)
+            for ref in ref_order:
+                t = ref_index[ref]
+                L = int(reference_lengths[ref])
+                results[ref], range_idx[ref] = _device_reference(
+                    ctx, fod.reads(t), L, mbq, ncols, k, nf, nf2, _mode,
+                    _tiles(ref) if _tiles else None, _tiles is not None)
+        err = _first_error(samfile, sel, ref_order, ref_index, reference_lengths, mbq,
+                           int(chunk_size), type_ord, range_idx)
+        if err is not None:
+            raise err
+        out = {}
+        for ref in ref_order:
+            t = ref_index[ref]
+            n = int(sel.ref_beg[t + 1] - sel.ref_beg[t])
+            if _mode == "rows":
+                out[ref] = {"rows": Rows(ref, results[ref], long_format), "num_reads": n}
+            else:
+                out[ref] = {"summary": results[ref], "num_reads": n,
+                            "length": int(reference_lengths[ref])}
+        return out
+    finally:
+        samfile.close()
+
+
+def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_tiles=False):
+    """Kernel 1 + kernel 2 (+ reductions) for one reference; returns (result, first bad read)."""
+    hist = ctx.alloc(max(4, 4 * ncols * L))
+    hist.zero()
+    if L > 0 or reads.n_reads > 0:
+        ctx.count(reads, L, mbq, ncols, hist.ptr)
+    bad = ctx.range_error()
+    if L == 0:
+        empty = RefData(np.zeros((k, 0), np.int32), np.zeros((k, 0)), np.zeros(0), np.zeros(0),
+                        np.zeros(0, np.int32))
+        return (empty if mode == "rows" else {"L": 0}), bad
+    outs = _alloc_outputs(ctx, k, L, want_pc=(mode == "rows"))
+    ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, outs["pc"].ptr if outs["pc"] else None,
+              outs["ent"].ptr, outs["sec"].ptr)
+    if mode == "rows":
+        counts = hist.download(np.int32, ncols * L).reshape(ncols, L)
+        return _download(outs, counts, k, L), bad
+    res = {"L": L}
+    work = ctx.alloc(D.summary_work_bytes(L))
+    dout = ctx.alloc(32)
+    ctx.summary(outs["cov"].ptr, outs["ent"].ptr, L, work.ptr, dout.ptr)
+    s = dout.download(np.float64, 4)
+    res.update(avg_cov=np.float64(s[0]), avg_ent=np.float64(s[1]), nnz=int(s[2]))
+    if tiles is not None and len(tiles):
+        lo = np.ascontiguousarray([a for a, _ in tiles], np.int64)
+        hi = np.ascontiguousarray([b for _, b in tiles], np.int64)
+        d_lo = ctx.alloc(lo.nbytes).upload(lo)
+        d_hi = ctx.alloc(hi.nbytes).upload(hi)
+        d_amp = ctx.alloc(48 * len(tiles))
+        ctx.amplicons(outs["cov"].ptr, outs["ent"].ptr, outs["sec"].ptr, L, d_lo.ptr, d_hi.ptr,
+                      len(tiles), d_amp.ptr)
+        amp = d_amp.download(np.float64, 6 * len(tiles)).reshape(-1, 6)
+        empty = [max(a, 0) > min(b, L - 1) for a, b in tiles]
+        res["amplicons"] = (amp, empty)
+    elif want_tiles:
+        res["amplicons"] = (np.zeros((0, 6)), [])
+    return res, bad
+
+
+class BaseCount:
+    """main.py:208-359."""
+
+    def __init__(self, bam, references=None, min_base_quality=0, min_mapping_quality=0,
+                 chunk_size=1000000, show_n_bases=False, long_format=False, *, device=None,
+                 _mode="rows", _tiles=None):
+        if long_format:
+            self.columns = ["reference", "position", "coverage", "base", "count", "percentage",
+                            "entropy", "secondary_entropy"]
+        else:
+            self.columns = ["reference", "position", "coverage", "num_a", "num_c", "num_g",
+                            "num_t", "num_ds", "num_n", "pc_a", "pc_c", "pc_g", "pc_t", "pc_ds",
+                            "pc_n", "entropy", "secondary_entropy"]
+            if not show_n_bases:
+                self.columns.pop(self.columns.index("num_n"))
+                self.columns.pop(self.columns.index("pc_n"))
+        self.data = get_basecounts(bam, references=references, min_base_quality=min_base_quality,
+                                   min_mapping_quality=min_mapping_quality, chunk_size=chunk_size,
+                                   show_n_bases=show_n_bases, long_format=long_format,
+                                   device=device, _mode=_mode, _tiles=_tiles)
+        self.references = list(self.data.keys())
+        if _mode == "rows":
+            self.reference_lengths = {ref: len(self.data[ref]["rows"]) for ref in self.references}
+        else:
+            self.reference_lengths = {ref: self.data[ref]["length"] for ref in self.references}
+
+    def _check(self, reference):
+        if self.data.get(reference) is None:
+            raise Exception(f"{reference} is not a valid reference")
+
+    def rows(self, reference=None):
+        if reference is None:
+            for ref in self.data.keys():
+                yield from self.data[ref]["rows"]
+        else:
+            self._check(reference)
+            yield from self.data[reference]["rows"]
+
+    def records(self, reference=None):
+        refs = list(self.data.keys()) if reference is None else [reference]
+        if reference is not None:
+            self._check(reference)
+        for ref in refs:
+            for row in self.data[ref]["rows"]:
+                yield dict(zip(self.columns, row))
+
+    def num_reads(self, reference=None):
+        if reference is None:
+            return sum([self.data[ref]["num_reads"] for ref in self.references])
+        self._check(reference)
+        return self.data[reference]["num_reads"]
+
+    def _arrays(self, reference):
+        refs = self.references if reference is None else [reference]
+        if reference is not None:
+            self._check(reference)
+        return [self.data[r]["rows"] for r in refs]
+
+    def mean_coverage(self, reference=None):
+        """np.mean over every row's coverage (long format repeats each position k times)."""
+        covs = []
+        for rows in self._arrays(reference):
+            c = rows.d.cov.astype(np.int64)
+            covs.append(np.repeat(c, rows.k) if rows.long else c)
+        return np.mean(np.concatenate(covs) if covs else np.zeros(0, np.int64))
+
+    def mean_entropy(self, reference=None, min_coverage=0):
+        ents = []
+        for rows in self._arrays(reference):
+            c = rows.d.cov.astype(np.int64)
+            e = rows.d.ent
+            if rows.long:
+                c, e = np.repeat(c, rows.k), np.repeat(e, rows.k)
+            ents.append(e[c >= min_coverage])
+        if not ents:
+            return np.mean([])
+        allv = np.concatenate(ents)
+        # an all-zero-coverage selection holds only int 1s in the reference: same mean
+        return np.mean(allv)
+
+
+def handle_arg(arg, name, default=None, provided_once=False):
+    """main.py:362-375."""
+    if arg is None:
+        return default
+    if provided_once:
+        if len(arg) > 1:
+            raise Exception(f"Argument --{name} can only be provided once")
+        return arg[0]
+    return list({a for a_list in arg for a in a_list})
+
+
+def build_parser() -> argparse.ArgumentParser:
+    """main.py:379-431, verbatim flags and help text."""
+    parser = argparse.ArgumentParser(prog="basecount")
+    parser.add_argument("bam", help="Path to BAM file (an index file is not required)")
+    parser.add_argument("-v", "--version", action="version", version=__version__)
+    parser.add_argument("--references", default=None, nargs="+", action="append",
+                        help="Choose specific reference(s) to run basecount on")
+    parser.add_argument("--min-base-quality", default=None, action="append",
+                        help="Default value: 0")
+    parser.add_argument("--min-mapping-quality", default=None, action="append",
+                        help="Default value: 0")
+    parser.add_argument("--chunk-size", default=None, action="append",
+                        help="Max number of reads loaded into memory and basecounted at a given "
+                             "time. Default value: 1000000")
+    parser.add_argument("--show-n-bases", default=False, action="store_true",
+                        help="Show counts of 'N' bases from reads, and include them in statistics")
+    group = parser.add_mutually_exclusive_group()
+    group.add_argument("--long-format", default=False, action="store_true",
+                       help="Output per-position statistics in long format, instead of the "
+                            "default wide format")
+    group.add_argument("--summarise", default=False, action="store_true",
+                       help="Output summary statistics")
+    group.add_argument("--summarise-with-bed", default=None, action="append", metavar="BED_FILE",
+                       help="Output summary statistics and amplicon vectors (calculated using the "
+                            "provided BED file)")
+    parser.add_argument("--decimal-places", default=None, action="append",
+                        help="Default value: 3")
+    return parser
+
+
+def _np_round_str(x, dp):
+    return str(round(x, dp))
+
+
+def run(argv=None):
+    """main.py:378-595: `basecount BAM [--long-format | --summarise | --summarise-with-bed BED]`."""
+    args = build_parser().parse_args(argv)
+    references = handle_arg(args.references, "references")
+    min_base_quality = int(handle_arg(args.min_base_quality, "min-base-quality", default=0,
+                                      provided_once=True))
+    min_mapping_quality = int(handle_arg(args.min_mapping_quality, "min-mapping-quality",
+                                         default=0, provided_once=True))
+    chunk_size = int(handle_arg(args.chunk_size, "chunk-size", default=1000000,
+                                provided_once=True))
+    bed = handle_arg(args.summarise_with_bed, "bed", provided_once=True)
+    decimal_places = int(handle_arg(args.decimal_places, "decimal_places", default=3,
+                                    provided_once=True))
+
+    if (not args.summarise) and (bed is None):
+        bc = BaseCount(args.bam, references=references, min_base_quality=min_base_quality,
+                       min_mapping_quality=min_mapping_quality, chunk_size=chunk_size,
+                       show_n_bases=args.show_n_bases, long_format=args.long_format)
+        print("\t".join(bc.columns))
+        for ref in bc.references:
+            rows = bc.data[ref]["rows"]
+            d = rows.d
+            fmt.write_bytes(fmt.rows_text(ref, d.counts[: rows.k], d.pc, d.ent, d.sec,
+                                          decimal_places, rows.long))
+        return
+
+    bed_errors = {}
+
+    def tiles(ref):
+        # the reference re-parses the BED for every reference (main.py:502), after printing that
+        # reference's summary: a bad BED is re-raised at that point of the output below
+        try:
+            scheme = load_scheme(bed)
+        except Exception as e:  # noqa: BLE001 - re-raised in output order
+            bed_errors[ref] = e
+            return None
+        return [(t[2]["inside_start"], t[2]["inside_end"]) for t in scheme]
+
+    bc = BaseCount(args.bam, references=references, min_base_quality=min_base_quality,
+                   min_mapping_quality=min_mapping_quality, chunk_size=chunk_size,
+                   show_n_bases=args.show_n_bases, long_format=args.long_format,
+                   _mode="summary", _tiles=tiles if bed is not None else None)
+    dp = decimal_places
+    for ref in bc.references:
+        s = bc.data[ref]["summary"]
+        ref_length = bc.reference_lengths[ref]
+        if ref_length == 0:
+            np.mean([])  # the reference's RuntimeWarning, then its ZeroDivisionError
+            raise ZeroDivisionError("division by zero")
+        pc_ref_coverage = 100 * (s["nnz"] / ref_length)
+        summary_stats = {
+            "reference_name": ref,
+            "reference_length": round(ref_length, dp),
+            "num_reads": round(bc.num_reads(ref), dp),
+            "pc_reference_coverage": round(pc_ref_coverage, dp),
+            "avg_depth": round(s["avg_cov"], dp),
+            "avg_entropy": round(s["avg_ent"], dp),
+        }
+        for name, val in summary_stats.items():
+            print(name, val, sep="\t")
+        if bed is not None:
+            if ref in bed_errors:
+                raise bed_errors[ref]
+            amp, empty = s["amplicons"]
+            vecs = [[] for _ in range(6)]
+            for i, e in enumerate(empty):
+                for j in range(6):
+                    vecs[j].append(-1 if e else np.float64(amp[i, j]))
+            names = ["mean_coverage_amplicon_vector", "median_coverage_amplicon_vector",
+                     "mean_entropy_amplicon_vector", "median_entropy_amplicon_vector",
+                     "mean_secondary_entropy_amplicon_vector",
+                     "median_secondary_entropy_amplicon_vector"]
+            for name, vec in zip(names, vecs):
+                val = ", ".join([_np_round_str(x, dp) for x in vec]) if vec else "-"
+                print(name, val, sep="\t")
+
+
+if __name__ == "__main__":
+    run()

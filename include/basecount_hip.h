@@ -1,0 +1,151 @@
+/*
+ * basecount_hip.h — C-ABI of the MI355X (gfx950) pileup counter.
+ *
+ * This is the drop-in boundary for the reference's only native operator:
+ *
+ *     count.bcount(refLen, minBaseQuality, reads, qualities, starts, ctuples)
+ *         -> list[list[int]]   (refLen x 6: A, C, G, T, DS, N)
+ *
+ *   defined at /root/reference/basecount/count.cpp:7-99, exported at count.cpp:102-105,
+ *   built as the top-level module `count` by /root/reference/setup.py:5 and called from
+ *   /root/reference/basecount/main.py:146-153 and :179-186,
+ *
+ * plus the per-position statistics the reference computes in Python right after it
+ * (get_stats / get_entropy, /root/reference/basecount/main.py:10-79) and the summary /
+ * amplicon reductions of main.py:469-595.
+ *
+ * Conventions
+ *   - Every function returns BC_OK (0) or a negative BC_E_* status; bc_last_error() gives the
+ *     message of the calling thread's last failure.
+ *   - Pointers named d_* are device (HBM) pointers, h_* are host pointers.  Device buffers passed
+ *     in are caller-owned; buffers created by bc_reads_upload()/bc_malloc() are library-owned and
+ *     released with bc_reads_free()/bc_free().
+ *   - Compute calls are stream-ordered and asynchronous on the context's stream; bc_sync() blocks.
+ *     No compute call allocates or synchronises, so a sequence of them can be captured into a
+ *     hipGraph (bc_graph_* below).
+ *   - Nothing here falls back to the CPU: without a gfx950 device, bc_ctx_create() fails.
+ */
+#ifndef BASECOUNT_HIP_H
+#define BASECOUNT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BC_OK 0
+#define BC_E_ARG (-1)   /* invalid argument (mirrors pybind11's TypeError on bad bcount args)   */
+#define BC_E_HIP (-2)   /* HIP runtime error                                                     */
+#define BC_E_RANGE (-3) /* a counted event fell outside [0, refLen) (count.cpp:60-65,85 .at())   */
+#define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
+
+#define BC_ABI_VERSION 1
+
+/* A batch of pre-decoded, accepted reads of ONE reference, struct-of-arrays.
+ * For read i (all fields as the reference's bcount sees them, count.cpp:22-38):
+ *   starts[i]  = pos[i]                              (0-based reference_start)
+ *   ctuples[i] = cigar[cig_beg[i] .. cig_beg[i]+cig_n[i])   BAM words: len << 4 | op
+ *   reads[i][j]     = SEQ nibble at index seq_nib[i] + j    ("=ACMGRSVTWYHKDBN" codes, packed
+ *                                                            two per byte, high nibble first)
+ *   qualities[i][j] = qual[seq_nib[i] + j]                  (qual is indexed by nibble index)
+ * i.e. seq_nib already includes the query_alignment_start (soft-clip) offset.
+ * The same struct describes host arrays (bc_reads_upload input, bc_bcount_host) and device
+ * arrays (bc_count input).                                                                     */
+typedef struct bc_reads {
+    int64_t n_reads;
+    const int32_t* pos;
+    const uint32_t* cig_beg;
+    const uint32_t* cig_n;
+    const uint32_t* seq_nib;
+    const uint32_t* cigar;
+    int64_t n_cigar_words;
+    const uint8_t* seq;
+    int64_t seq_bytes;
+    const uint8_t* qual;      /* may be NULL; then minBaseQuality must be 0                    */
+    int64_t qual_bytes;       /* >= 2*seq_bytes when qual != NULL                              */
+    int32_t sorted;           /* 1 if pos[] is non-decreasing (enables the LDS-window kernel)  */
+    int32_t max_span;         /* max reference span of any read (0 = unknown -> computed)      */
+} bc_reads;
+
+typedef struct bc_ctx bc_ctx;
+
+const char* bc_last_error(void);
+int bc_abi_version(void);
+int bc_device_count(int* n);
+
+/* Create a context on `device`.  `stream` is a hipStream_t (NULL: the library creates and owns
+ * a non-blocking stream).  The context holds only small scratch state (the range-error word).   */
+int bc_ctx_create(int device, void* stream, bc_ctx** out);
+int bc_ctx_destroy(bc_ctx* ctx);
+int bc_ctx_stream(bc_ctx* ctx, void** stream);
+int bc_sync(bc_ctx* ctx);
+
+/* Library-owned device memory helpers (for hosts without another allocator). */
+int bc_malloc(bc_ctx* ctx, size_t bytes, void** d_ptr);
+int bc_free(bc_ctx* ctx, void* d_ptr);
+int bc_memcpy_h2d(bc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);  /* async */
+int bc_memcpy_d2h(bc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);  /* async */
+int bc_memset(bc_ctx* ctx, void* d_dst, int value, size_t bytes);              /* async */
+
+/* Copy a host batch to HBM (library-owned); computes max_span when the host left it 0. */
+int bc_reads_upload(bc_ctx* ctx, const bc_reads* h_reads, bc_reads* d_reads);
+int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
+
+/* Kernel 1 — CIGAR-expand + scatter-add (count.cpp:22-97).
+ * Accumulates into d_hist, an int32 histogram of `ncols` planes of `ref_len` positions
+ * (plane-major: d_hist[c * ref_len + p]).  ncols = 6 gives the reference's full layout
+ * (A,C,G,T,DS,N); ncols = 5 drops N (main.py:19-31 never uses it unless show_n_bases).
+ * M/=/X bases with qual >= min_base_quality count A/C/G/T/N; other letters count nowhere;
+ * I advances the read; D/N-skip count DS with no quality test; S/H/P/B are no-ops.
+ * A counted event at position >= ref_len is recorded (first offending read index kept);
+ * read it with bc_range_error().  Async; does not zero d_hist.                               */
+int bc_count(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality,
+             int ncols, int32_t* d_hist);
+
+/* Blocking: returns the smallest read index that produced an out-of-range counted event since
+ * the last call (or -1) and clears the record.                                                 */
+int bc_range_error(bc_ctx* ctx, int64_t* first_bad_read);
+
+/* Kernel 2 — per-position statistics (main.py:14-79), fp64, same operation order as CPython:
+ *   cov = sum(c);  pc_j = 100 * (c_j / cov);  H = nf * sum_j -(p_j*log2(p_j)) [p_j != 0];
+ *   H2 = nf2 * (same over the counts with the first argmax removed, over cov - max).
+ * k = 5 (A,C,G,T,DS) or 6 (+N, show_n_bases); planes 0..k-1 of d_hist are used.
+ * Outputs (device, caller-owned; any of d_pc / d_ent / d_sec may be NULL to skip):
+ *   d_cov [L] int32, d_pc [k][L] f64, d_ent [L] f64, d_sec [L] f64.
+ * Where cov == 0 the reference emits ints (-1 / 1 / 1): here pc = -1.0, H = H2 = 1.0.
+ * Where cov2 == 0 the reference emits int 1 for H2: here 1.0.                                 */
+int bc_stats(bc_ctx* ctx, const int32_t* d_hist, int64_t ref_len, int k, double nf, double nf2,
+             int32_t* d_cov, double* d_pc, double* d_ent, double* d_sec);
+
+/* Summary reductions of one reference (main.py:469-495), bit-identical to numpy:
+ *   out[0] = np.mean(coverages)     out[1] = np.mean(entropies)
+ *   out[2] = number of positions with coverage != 0 (as double, exact)
+ *   out[3] = sum of coverages (exact, as double when < 2^53)
+ * numpy's float64 add.reduce is emulated exactly: 8192-element buffer chunks added left to right,
+ * each chunk summed by numpy's pairwise_sum (8-way unrolled leaves of <= 128).  d_out: 4 doubles,
+ * device memory.  d_work must hold bc_summary_work_bytes(ref_len) bytes.                     */
+size_t bc_summary_work_bytes(int64_t ref_len);
+int bc_summary(bc_ctx* ctx, const int32_t* d_cov, const double* d_ent, int64_t ref_len,
+               void* d_work, double* d_out);
+
+/* Amplicon vectors (main.py:501-551): for each tile t with inclusive window
+ * [lo[t], hi[t]] (already clipped to [0, ref_len-1]; lo > hi = empty), np.mean and np.median of
+ * coverage, entropy and secondary entropy over the window.  d_out: [n_tiles][6] f64 device
+ * (mean_cov, median_cov, mean_ent, median_ent, mean_sec, median_sec); empty tiles give -1.0. */
+int bc_amplicons(bc_ctx* ctx, const int32_t* d_cov, const double* d_ent, const double* d_sec,
+                 int64_t ref_len, const int64_t* d_lo, const int64_t* d_hi, int32_t n_tiles,
+                 double* d_out);
+
+/* Drop-in for count.bcount with host buffers: uploads, counts all 6 columns, downloads.
+ * h_out: refLen x 6 uint32, ROW-major like the reference's vector<vector<unsigned>>
+ * (h_out[p*6 + c]).  On BC_E_RANGE, *bad_read / *bad_pos give the first offending read (in
+ * read order) and the refPos the reference's .at() would have rejected (count.cpp:60-65,85). */
+int bc_bcount_host(int device, int64_t ref_len, uint32_t min_base_quality, const bc_reads* h_reads,
+                   uint32_t* h_out, int64_t* bad_read, int64_t* bad_pos);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -29,6 +29,23 @@ int hip_fail(hipError_t e, const char* where) {
         if (_e != hipSuccess) return hip_fail(_e, #expr); \
     } while (0)
 
+// hipEvents around one launch when the context's timing is on
+struct Timed {
+    bc_ctx* c;
+    int id;
+    hipEvent_t a = nullptr, b = nullptr;
+    Timed(bc_ctx* ctx, int kid) : c(ctx), id(kid) {
+        if (c->timing && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+            (void)hipEventRecord(a, c->stream);
+    }
+    ~Timed() {
+        if (a && b) {
+            (void)hipEventRecord(b, c->stream);
+            c->ev[id].emplace_back(a, b);
+        }
+    }
+};
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -61,8 +78,10 @@ bool host_sorted(const int32_t* pos, int64_t n) {
     return true;
 }
 
-int host_max_span(const bc_reads& r) {
+// max reference span and max read end (pos + span) of a host batch
+std::pair<int, int64_t> host_spans(const bc_reads& r) {
     uint64_t best = 0;
+    int64_t end = 0;
     for (int64_t i = 0; i < r.n_reads; ++i) {
         const uint32_t* cg = r.cigar + r.cig_beg[i];
         uint64_t span = 0;
@@ -71,8 +90,9 @@ int host_max_span(const bc_reads& r) {
             if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) span += cg[k] >> 4;
         }
         best = std::max(best, span);
+        end = std::max<int64_t>(end, (int64_t)r.pos[i] + (int64_t)span);
     }
-    return (int)std::min<uint64_t>(best, 0x7fffffff);
+    return {(int)std::min<uint64_t>(best, 0x7fffffff), end};
 }
 
 int check_host_reads(const bc_reads* r) {
@@ -180,6 +200,11 @@ int bc_ctx_destroy(bc_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->h_err) (void)hipHostFree(c->h_err);
+    for (auto& v : c->ev)
+        for (auto& pr : v) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return BC_OK;
@@ -250,8 +275,11 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     d->n_cigar_words = h->n_cigar_words;
     d->seq_bytes = h->seq_bytes;
     d->qual_bytes = h->qual ? h->qual_bytes : 0;
-    d->sorted = h->n_reads ? (h->sorted ? 1 : (host_sorted(h->pos, h->n_reads) ? 1 : 0)) : 1;
-    d->max_span = h->max_span > 0 ? h->max_span : (h->n_reads ? host_max_span(*h) : 0);
+    // the tiled kernel relies on both properties: always derive them from the data itself
+    d->sorted = h->n_reads ? (host_sorted(h->pos, h->n_reads) ? 1 : 0) : 1;
+    const auto sp = h->n_reads ? host_spans(*h) : std::pair<int, int64_t>(0, 0);
+    d->max_span = sp.first;
+    d->max_end = sp.second;
     const size_t n = (size_t)h->n_reads;
     void* p[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     const size_t sz[7] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4, (size_t)h->seq_bytes,
@@ -297,8 +325,95 @@ int bc_count(bc_ctx* c, const bc_reads* r, int64_t ref_len, uint32_t mbq, int nc
     if (!d_hist && ref_len > 0) return fail(BC_E_ARG, "d_hist is NULL");
     if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
     DeviceGuard g(c->device);
+    if (r->sorted && r->max_span <= bc::kTileMaxSpan) {
+        // sorted batch: the tiled kernel in accumulate mode (plain read-add-write per owned tile)
+        Timed tm(c, BC_K_PILEUP);
+        HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, ref_len, r->max_end, mbq, ncols, false, true, 0.0, 0.0,
+                                        d_hist, nullptr, nullptr, nullptr, nullptr, c->d_err));
+        return BC_OK;
+    }
     const int rpb = choose_rpb(r->n_reads, ref_len, r->max_span, r->sorted);
+    Timed tm(c, BC_K_COUNT);
     HIP_TRY(bc::launch_count(c->stream, *r, ref_len, mbq, ncols, d_hist, rpb, c->d_err));
+    return BC_OK;
+}
+
+int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, double nf, double nf2, int32_t* d_counts,
+              int32_t* d_cov, double* d_pc, double* d_ent, double* d_sec) {
+    if (!c || !r) return fail(BC_E_ARG, "NULL argument");
+    if (k != 5 && k != 6) return fail(BC_E_ARG, "k must be 5 or 6");
+    if (L < 0) return fail(BC_E_ARG, "ref_len < 0");
+    if (!r->sorted) return fail(BC_E_ARG, "bc_pileup needs a coordinate-sorted batch (sorted == 1)");
+    if (r->max_span > bc::kTileMaxSpan)
+        return fail(BC_E_ARG, "bc_pileup: max_span above 4096; use bc_count + bc_stats");
+    if (mbq > 0 && r->n_reads > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+    if (L > 0 && (!d_counts || !d_cov || !d_ent || !d_sec)) return fail(BC_E_ARG, "NULL output");
+    DeviceGuard g(c->device);
+    Timed tm(c, BC_K_PILEUP);
+    HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, d_counts, d_cov,
+                                    d_pc, d_ent, d_sec, c->d_err));
+    return BC_OK;
+}
+
+int bc_graph_begin(bc_ctx* c) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (!c->stream) return fail(BC_E_ARG, "cannot capture the legacy default stream");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    return BC_OK;
+}
+
+int bc_graph_end(bc_ctx* c, bc_graph** out) {
+    if (!c || !out) return fail(BC_E_ARG, "NULL argument");
+    DeviceGuard g(c->device);
+    auto* gr = new bc_graph();
+    hipError_t e = hipStreamEndCapture(c->stream, &gr->graph);
+    if (e == hipSuccess) e = hipGraphInstantiate(&gr->exec, gr->graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        bc_graph_destroy(gr);
+        return hip_fail(e, "graph capture");
+    }
+    *out = gr;
+    return BC_OK;
+}
+
+int bc_graph_launch(bc_ctx* c, bc_graph* gr) {
+    if (!c || !gr) return fail(BC_E_ARG, "NULL argument");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipGraphLaunch(gr->exec, c->stream));
+    return BC_OK;
+}
+
+int bc_graph_destroy(bc_graph* gr) {
+    if (!gr) return BC_OK;
+    if (gr->exec) (void)hipGraphExecDestroy(gr->exec);
+    if (gr->graph) (void)hipGraphDestroy(gr->graph);
+    delete gr;
+    return BC_OK;
+}
+
+int bc_timing_enable(bc_ctx* c, int on) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    c->timing = on != 0;
+    return BC_OK;
+}
+
+int bc_timing_report(bc_ctx* c, int64_t* launches, double* mean_us) {
+    if (!c || !launches || !mean_us) return fail(BC_E_ARG, "NULL argument");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int id = 0; id < BC_KERNEL_IDS; ++id) {
+        double tot = 0.0;
+        for (auto& pr : c->ev[id]) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) tot += ms;
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+        launches[id] = (int64_t)c->ev[id].size();
+        mean_us[id] = c->ev[id].empty() ? 0.0 : tot * 1e3 / (double)c->ev[id].size();
+        c->ev[id].clear();
+    }
     return BC_OK;
 }
 
@@ -320,6 +435,7 @@ int bc_stats(bc_ctx* c, const int32_t* d_hist, int64_t L, int k, double nf, doub
     if (L == 0) return BC_OK;
     if (!d_hist) return fail(BC_E_ARG, "d_hist is NULL");
     DeviceGuard g(c->device);
+    Timed tm(c, BC_K_STATS);
     HIP_TRY(bc::launch_stats(c->stream, d_hist, L, k, nf, nf2, d_cov, d_pc, d_ent, d_sec));
     return BC_OK;
 }
@@ -331,6 +447,7 @@ int bc_summary(bc_ctx* c, const int32_t* d_cov, const double* d_ent, int64_t L, 
     if (L <= 0) return fail(BC_E_ARG, "ref_len must be > 0 (np.mean of an empty list)");
     if (!d_cov || !d_ent) return fail(BC_E_ARG, "NULL coverage / entropy");
     DeviceGuard g(c->device);
+    Timed tm(c, BC_K_SUMMARY);
     HIP_TRY(bc::launch_summary(c->stream, d_cov, d_ent, L, d_work, d_out));
     return BC_OK;
 }
@@ -342,6 +459,7 @@ int bc_amplicons(bc_ctx* c, const int32_t* d_cov, const double* d_ent, const dou
     if (n_tiles == 0) return BC_OK;
     if (!d_cov || !d_ent || !d_sec || !d_lo || !d_hi || !d_out) return fail(BC_E_ARG, "NULL argument");
     DeviceGuard g(c->device);
+    Timed tm(c, BC_K_AMPLICONS);
     HIP_TRY(bc::launch_amplicons(c->stream, d_cov, d_ent, d_sec, L, d_lo, d_hi, n_tiles, d_out));
     return BC_OK;
 }

@@ -2,8 +2,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "basecount_hip.h"
 
@@ -13,6 +17,13 @@ struct bc_ctx {
     bool own_stream = false;
     unsigned long long* d_err = nullptr;  // first out-of-range read index (atomicMin), ~0 = none
     unsigned long long* h_err = nullptr;  // pinned mirror
+    bool timing = false;                  // bc_timing_enable: hipEvents around every launch
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[BC_KERNEL_IDS];
+};
+
+struct bc_graph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
 };
 
 namespace bc {
@@ -31,6 +42,10 @@ hipError_t launch_count(hipStream_t s, const bc_reads& r, int64_t ref_len, uint3
 hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span);
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2,
                         int32_t* cov, double* pc, double* ent, double* sec);
+hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
+                               bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
+                               double* pc, double* ent, double* sec, unsigned long long* d_err);
+constexpr int kTileMaxSpan = 4096;  // beyond this span the tiled kernel's look-back gets too long
 size_t summary_work_bytes(int64_t L);
 hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
                           double* out);

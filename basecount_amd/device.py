@@ -15,6 +15,8 @@ import numpy as np
 from ._native import _libs, _load
 
 BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV = -1, -2, -3, -4
+KERNEL_NAMES = ("count", "stats", "reserved", "pileup", "summary", "amplicons")  # BC_K_* ids
+KERNEL_IDS = len(KERNEL_NAMES)
 
 
 class BcReads(C.Structure):
@@ -32,6 +34,7 @@ class BcReads(C.Structure):
         ("qual_bytes", C.c_int64),
         ("sorted", C.c_int32),
         ("max_span", C.c_int32),
+        ("max_end", C.c_int64),
     ]
 
 
@@ -70,6 +73,14 @@ def lib() -> C.CDLL:
         "bc_amplicons": ([vp, vp, vp, vp, i64, vp, vp, C.c_int32, vp], C.c_int),
         "bc_bcount_host": ([C.c_int, i64, u32, C.POINTER(BcReads), vp, C.POINTER(i64),
                             C.POINTER(i64)], C.c_int),
+        "bc_pileup": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, dbl, dbl, vp, vp, vp, vp, vp],
+                      C.c_int),
+        "bc_graph_begin": ([vp], C.c_int),
+        "bc_graph_end": ([vp, C.POINTER(vp)], C.c_int),
+        "bc_graph_launch": ([vp, vp], C.c_int),
+        "bc_graph_destroy": ([vp], C.c_int),
+        "bc_timing_enable": ([vp, C.c_int], C.c_int),
+        "bc_timing_report": ([vp, vp, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -209,6 +220,33 @@ class Context:
         r = reads.r if isinstance(reads, DeviceReads) else reads
         check(lib().bc_count(self.h, C.byref(r), int(ref_len), int(mbq), int(ncols), d_hist))
 
+    def pileup(self, reads, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec):
+        """Fused kernel 1 + kernel 2 (bc_pileup) for a coordinate-sorted batch: one launch."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        check(lib().bc_pileup(self.h, C.byref(r), int(L), int(mbq), int(k), float(nf), float(nf2),
+                              d_counts, d_cov, d_pc, d_ent, d_sec))
+
+    def capture(self, fn) -> "Graph":
+        """Record the compute calls made by fn() into a hipGraph (replay with Graph.launch)."""
+        check(lib().bc_graph_begin(self.h))
+        try:
+            fn()
+        finally:
+            g = C.c_void_p()
+            rc = lib().bc_graph_end(self.h, C.byref(g))
+        check(rc)
+        return Graph(self, g.value)
+
+    def timing(self, on: bool = True) -> None:
+        check(lib().bc_timing_enable(self.h, int(bool(on))))
+
+    def timing_report(self) -> dict:
+        """{kernel: (launches, mean_us)} since the last report (synchronises)."""
+        n = np.zeros(KERNEL_IDS, np.int64)
+        us = np.zeros(KERNEL_IDS, np.float64)
+        check(lib().bc_timing_report(self.h, n.ctypes.data, us.ctypes.data))
+        return {name: (int(n[i]), float(us[i])) for i, name in enumerate(KERNEL_NAMES) if n[i]}
+
     def range_error(self) -> int:
         v = C.c_int64(-1)
         check(lib().bc_range_error(self.h, C.byref(v)))
@@ -224,6 +262,22 @@ class Context:
     def amplicons(self, d_cov, d_ent, d_sec, L, d_lo, d_hi, n_tiles, d_out) -> None:
         check(lib().bc_amplicons(self.h, d_cov, d_ent, d_sec, int(L), d_lo, d_hi, int(n_tiles),
                                  d_out))
+
+
+class Graph:
+    def __init__(self, ctx: Context, h: int):
+        self.ctx, self.h = ctx, h
+
+    def launch(self):
+        check(lib().bc_graph_launch(self.ctx.h, self.h))
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().bc_graph_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
 
 
 def summary_work_bytes(L: int) -> int:

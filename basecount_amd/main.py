@@ -359,6 +359,7 @@ class _FileOnDevice:
         pos = self.pos[b0:b1]
         r.sorted = int(bool(np.all(pos[1:] >= pos[:-1]))) if b1 - b0 > 1 else 1
         r.max_span = int(min(self.span[b0:b1].max(), 2**31 - 1)) if b1 > b0 else 0
+        r.max_end = int((pos.astype(np.int64) + self.span[b0:b1]).max()) if b1 > b0 else 0
         return r
 
 
@@ -417,19 +418,31 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
 
 
 def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_tiles=False):
-    """Kernel 1 + kernel 2 (+ reductions) for one reference; returns (result, first bad read)."""
-    hist = ctx.alloc(max(4, 4 * ncols * L))
-    hist.zero()
-    if L > 0 or reads.n_reads > 0:
-        ctx.count(reads, L, mbq, ncols, hist.ptr)
-    bad = ctx.range_error()
+    """Kernel 1 + kernel 2 (+ reductions) for one reference; returns (result, first bad read).
+
+    Coordinate-sorted batches take the fused tiled kernel (bc_pileup); others count with the
+    event-parallel kernel (bc_count) and then run kernel 2 (bc_stats)."""
     if L == 0:
+        if reads.n_reads > 0:
+            hist = ctx.alloc(4 * ncols)
+            hist.zero()
+            ctx.count(reads, 0, mbq, ncols, hist.ptr)
+        bad = ctx.range_error()
         empty = RefData(np.zeros((k, 0), np.int32), np.zeros((k, 0)), np.zeros(0), np.zeros(0),
                         np.zeros(0, np.int32))
         return (empty if mode == "rows" else {"L": 0}), bad
     outs = _alloc_outputs(ctx, k, L, want_pc=(mode == "rows"))
-    ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, outs["pc"].ptr if outs["pc"] else None,
-              outs["ent"].ptr, outs["sec"].ptr)
+    hist = ctx.alloc(4 * ncols * L)
+    pc_ptr = outs["pc"].ptr if outs["pc"] else None
+    if reads.sorted and reads.max_span <= 4096:
+        ctx.pileup(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
+                   outs["sec"].ptr)
+    else:
+        hist.zero()
+        ctx.count(reads, L, mbq, ncols, hist.ptr)
+        ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
+                  outs["sec"].ptr)
+    bad = ctx.range_error()
     if mode == "rows":
         counts = hist.download(np.int32, ncols * L).reshape(ncols, L)
         return _download(outs, counts, k, L), bad

@@ -1,0 +1,244 @@
+"""Benchmark: reference positions/sec of the pileup hot path on MI355X.
+
+A step = one pass of the hot path over one batch already resident in HBM: zero the histogram,
+kernel 1 (CIGAR-expand + scatter-add, count.cpp:22-97), kernel 2 (per-position statistics,
+main.py:29-78).  Workload at N=1: BASELINE config 2 (1 contig 29,903 bp, 100,000 reads x 150 bp,
+all-M CIGAR).  At N>1 every rank runs its own contig of that shape (contig sharding, weak
+scaling, no collective inside the step); the per-contig results are gathered to rank 0 over
+RCCL once after the timed region (reported as gather_ms).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    "c2": "C2: 1 contig 29,903 bp, 100,000 reads x 150 bp, all-M CIGAR (per rank)",
+    "c3": "C3: 1 contig 29,903 bp, 1,000,000 reads x 150 bp, mixed M/I/D/=/X/S CIGAR (per rank)",
+}
+
+
+def kernel1_bytes(b: dict, L: int, ncols: int, mbq: int, l_seq: np.ndarray) -> int:
+    """Algorithmic HBM bytes of one kernel-1 launch: per read 16 B of
+    read index (pos, cig_beg, cig_n, seq_nib) + 4 B per CIGAR word + ceil(l_seq/2) B of packed
+    SEQ (+ l_seq B of QUAL when mbq > 0), plus the 4*ncols*L histogram written once."""
+    n = int(b["pos"].size)
+    per_read = 16 * n + 4 * int(b["cig_n"].sum()) + int(((l_seq + 1) // 2).sum())
+    if mbq > 0:
+        per_read += int(l_seq.sum())
+    return per_read + 4 * ncols * L
+
+
+def cpu_baseline(rs, b, L: int, budget_s: float = 10.0) -> dict:
+    """The reference's CPU path on the same workload: its own compiled count.bcount (oracle/_ref,
+    pybind11, Python-list arguments as main.py:146 passes them) + get_stats (main.py:14-79,
+    restated in oracle.get_stats_py).  Single thread, like the reference."""
+    import oracle as O
+
+    ref = O.ref_bcount()
+    n = int(b["pos"].size)
+    if ref is not None:
+        # pysam-shaped arguments (built once, untimed): clipped strings, qualities, starts, tuples
+        seqs = rs.seq.reshape(n, -1)
+        nt = np.frombuffer(b"=ACMGRSVTWYHKDBN", np.uint8)
+        codes = np.empty((n, seqs.shape[1] * 2), np.uint8)
+        codes[:, 0::2], codes[:, 1::2] = seqs >> 4, seqs & 15
+        reads = [bytes(nt[row]).decode() for row in codes]
+        quals = [q for q in rs.qual.reshape(n, -1).tolist()]
+        starts = b["pos"].tolist()
+        ctuples = [[(0, 150)]] * n
+        done, t0 = 0, time.perf_counter()
+        while True:
+            counts = ref(L, 0, reads, quals, starts, ctuples)
+            O.get_stats_py(counts, "ref")
+            done += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        dt = (time.perf_counter() - t0) / done
+        kind, what = "reference", ("reference count.cpp (pybind11 bcount, list arguments) + "
+                                   "get_stats main.py:14-79 (Python)")
+    else:
+        done, t0 = 0, time.perf_counter()
+        while True:
+            counts, _ = O.bcount(L, 0, b)
+            O.stats(counts, False)
+            done += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        dt = (time.perf_counter() - t0) / done
+        kind, what = "port", "oracle C restatement of bcount + get_stats"
+    return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind,
+            "sample": f"{what}; full C2 workload ({n} reads, {L} positions) x {done} runs, "
+                      f"{dt * 1e3:.1f} ms per run, BAM decode excluded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--mbq", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = torch = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from basecount_amd import device as D
+    from basecount_amd import synth
+    from basecount_amd.main import norm_factors
+
+    # ---- workload: this rank's contig (weak scaling: one contig per rank) --------------------
+    name = "MN908947.3" if world == 1 else f"contig{rank}"
+    c = synth.CONFIGS[args.config]
+    rs = synth.make_reads([(name, c["contigs"][0][1])], c["reads"], c["mixed"],
+                          c["seed"] + 1000 * rank)
+    b = synth.batch_arrays(rs, 0, 0)
+    L = rs.lengths[0]
+    ncols = k = 5
+    ctx = D.Context(local if world > 1 else 0)  # library-owned non-blocking stream
+    reads = D.DeviceReads(ctx, b)               # resident in HBM before anything is timed
+    assert reads.r.sorted == 1
+    counts = ctx.alloc(4 * ncols * L)
+    dcov, dpc, dent, dsec = ctx.alloc(4 * L), ctx.alloc(8 * k * L), ctx.alloc(8 * L), ctx.alloc(8 * L)
+    nf, nf2 = norm_factors(k)
+
+    def step():
+        # one pass of the hot path: fused CIGAR-expand/count + statistics, one launch
+        ctx.pileup(reads, L, args.mbq, k, nf, nf2, counts.ptr, dcov.ptr, dpc.ptr, dent.ptr,
+                   dsec.ptr)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    assert ctx.range_error() == -1
+    graph = ctx.capture(step)   # the step as a hipGraph (one kernel node)
+    for _ in range(args.warmup):
+        graph.launch()
+    ctx.sync()
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    # ---- timed region: K replays of the step, bracketed by barrier + device sync ------------
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        graph.launch()
+    ctx.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-kernel durations: hipEvents on the library stream around each launch -----------
+    ctx.timing(True)
+    for _ in range(args.steps):
+        step()
+    rep = ctx.timing_report()
+    ctx.timing(False)
+    k1 = rep["pileup"][1] * 1e-6
+
+    # ---- correctness of what was timed (rank-local): counts vs the oracle -------------------
+    got = counts.download(np.int32, ncols * L).reshape(ncols, L)
+    import oracle as O
+
+    exp, _ = O.bcount(L, args.mbq, b)
+    parity = bool(np.array_equal(got, exp[:, :ncols].T.astype(np.int32)))
+    _, _, oent, _ = O.stats(exp, False)
+    parity = parity and float(np.max(np.abs(dent.download(np.float64, L) - oent))) <= 1e-6
+
+    # ---- gather per-contig coverage to rank 0 over RCCL (output step, outside the timing) ----
+    gather_ms = None
+    if dist:
+        covt = torch.from_numpy(dcov.download(np.int32, L)).cuda()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        bufs = [torch.zeros_like(covt) for _ in range(world)] if rank == 0 else None
+        dist.gather(covt, bufs, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) * 1e3
+
+    events = synth.ref_events(rs)
+    ms = elapsed / args.steps * 1e3
+    positions = world * L * args.steps
+    kbytes = kernel1_bytes(b, L, ncols, args.mbq, rs.l_seq)
+    achieved = kbytes / k1 / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "kernel1_pmc.json")
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            pm = json.load(fh)
+        if pm.get("config") == args.config and pm.get("mbq", 0) == args.mbq:
+            traffic = pm.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(rs, b, L, args.cpu_budget)
+        value = positions / elapsed
+        line = {
+            "metric": "reference positions/sec (kernel 1 + kernel 2, inputs resident in HBM)",
+            "value": value,
+            "unit": "positions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32 counts / f64 stats",
+            "data": "synthetic (seeded, BASELINE config shape)",
+            "config": {"workload": WORKLOADS[args.config], "reads_per_rank": int(b["pos"].size),
+                       "positions_per_rank": L, "min_base_quality": args.mbq,
+                       "parallelism": f"contig-sharded x{world}"},
+            "gbases_piled_per_s": world * events * args.steps / elapsed / 1e9,
+            "pileup_kernel_us": k1 * 1e6,
+            "kernels": "k_pileup (kernel 1 and kernel 2 fused, one launch), hipGraph replay",
+            "parity_vs_oracle": parity,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_pileup (fused kernel 1 + 2)", "algorithmic_bytes": kbytes},
+            "cpu_baseline": cpu,
+            "gather_ms": gather_ms,
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = value / cpu["value"]
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    if not parity:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

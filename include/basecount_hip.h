@@ -65,8 +65,9 @@ typedef struct bc_reads {
     int64_t seq_bytes;
     const uint8_t* qual;      /* may be NULL; then minBaseQuality must be 0                    */
     int64_t qual_bytes;       /* >= 2*seq_bytes when qual != NULL                              */
-    int32_t sorted;           /* 1 if pos[] is non-decreasing (enables the LDS-window kernel)  */
-    int32_t max_span;         /* max reference span of any read (0 = unknown -> computed)      */
+    int32_t sorted;           /* 1 if pos[] is non-decreasing (enables the tiled kernel)       */
+    int32_t max_span;         /* upper bound of every read's reference span (M/D/N/=/X bases)  */
+    int64_t max_end;          /* upper bound of pos[i] + span[i] over the batch                */
 } bc_reads;
 
 typedef struct bc_ctx bc_ctx;
@@ -89,7 +90,9 @@ int bc_memcpy_h2d(bc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);  /
 int bc_memcpy_d2h(bc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);  /* async */
 int bc_memset(bc_ctx* ctx, void* d_dst, int value, size_t bytes);              /* async */
 
-/* Copy a host batch to HBM (library-owned); computes max_span when the host left it 0. */
+/* Copy a host batch to HBM (library-owned).  `sorted` and `max_span` of the device batch are
+ * derived from the data (the host's values are ignored).  For batches assembled directly in
+ * device memory the caller must set both truthfully: the tiled kernel trusts them.           */
 int bc_reads_upload(bc_ctx* ctx, const bc_reads* h_reads, bc_reads* d_reads);
 int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
 
@@ -103,6 +106,41 @@ int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
  * read it with bc_range_error().  Async; does not zero d_hist.                               */
 int bc_count(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality,
              int ncols, int32_t* d_hist);
+
+/* Fused kernel 1 + kernel 2 — the hot path in ONE launch.  For a coordinate-sorted batch
+ * (d_reads->sorted == 1, max_span <= 4096, max_end truthful) the reference is cut into
+ * 64-position tiles; each tile finds its reads by a search over pos[], walks them with lanes
+ * owning positions and register counters (no atomics, no histogram memset), and writes
+ *   d_counts [k][L] int32 (the reference's baseCounts columns, N only when k == 6),
+ *   d_cov, d_pc (may be NULL), d_ent, d_sec  exactly as bc_stats defines them.
+ * Out-of-range counted events are recorded for bc_range_error() as with bc_count.
+ * Overwrites its outputs; async; capturable.                                                   */
+int bc_pileup(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality, int k,
+              double nf, double nf2, int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent,
+              double* d_sec);
+
+/* hipGraph capture of a sequence of compute calls on the context's stream (the context must own
+ * its stream or have been given a non-default one).  bc_graph_end instantiates the graph;
+ * bc_graph_launch replays it on the context's stream.                                         */
+typedef struct bc_graph bc_graph;
+int bc_graph_begin(bc_ctx* ctx);
+int bc_graph_end(bc_ctx* ctx, bc_graph** out);
+int bc_graph_launch(bc_ctx* ctx, bc_graph* g);
+int bc_graph_destroy(bc_graph* g);
+
+/* Per-kernel timing (SURVEY §5 tracing): when enabled, every launch made through the context is
+ * bracketed by hipEvents on its stream.  bc_timing_report() synchronises and returns, per kernel
+ * id (BC_K_*), the number of timed launches and their mean duration in microseconds, then clears
+ * the record.  Do not enable while capturing a graph.                                          */
+#define BC_K_COUNT 0      /* event-parallel kernel 1 (unsorted / long-span batches) */
+#define BC_K_STATS 1      /* kernel 2                                              */
+#define BC_K_RESERVED 2   /* (unused)                                              */
+#define BC_K_PILEUP 3     /* fused tiled kernel 1 + 2                              */
+#define BC_K_SUMMARY 4
+#define BC_K_AMPLICONS 5
+#define BC_KERNEL_IDS 6
+int bc_timing_enable(bc_ctx* ctx, int on);
+int bc_timing_report(bc_ctx* ctx, int64_t* launches /* [BC_KERNEL_IDS] */, double* mean_us /* [..] */);
 
 /* Blocking: returns the smallest read index that produced an out-of-range counted event since
  * the last call (or -1) and clears the record.                                                 */

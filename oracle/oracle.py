@@ -225,17 +225,16 @@ def split_blocks(text: str, summary_mode: bool):
     """Output text -> (header, {reference: block}) so multi-reference outputs can be compared
     independently of the set iteration order (main.py:92)."""
     lines = text.splitlines(keepends=True)
-    blocks, header = {}, ""
+    parts, header = {}, ""
     if summary_mode:
         cur = None
         for ln in lines:
             if ln.startswith("reference_name\t"):
                 cur = ln.split("\t", 1)[1].rstrip("\n")
-                blocks[cur] = ""
-            blocks[cur] += ln
-        return header, blocks
-    header = lines[0] if lines else ""
-    for ln in lines[1:]:
-        ref = ln.split("\t", 1)[0]
-        blocks[ref] = blocks.get(ref, "") + ln
-    return header, blocks
+                parts[cur] = []
+            parts[cur].append(ln)
+    else:
+        header = lines[0] if lines else ""
+        for ln in lines[1:]:
+            parts.setdefault(ln.split("\t", 1)[0], []).append(ln)
+    return header, {k: "".join(v) for k, v in parts.items()}

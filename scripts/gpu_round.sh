@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: smoke -> gpu tests -> bench -> rocprof kernel trace.  Stops at the first
+# fault / abort / timeout (exit 124, 134, 137, 139) so a broken kernel never runs twice.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STEPS="${STEPS:-smoke tests bench prof}"
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" ; date
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -5 "gpurun_out/$name.log"
+  if fatal $rc; then echo "FATAL in $name, stopping"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 1200 python -m pytest tests -m gpu -x -q -s ${PYTEST_ARGS} ;;
+    bench) run bench 600 python bench.py ${BENCH_ARGS} ;;
+    prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+           run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --steps 200 ${BENCH_ARGS} ;;
+  esac
+done
+echo ALLDONE

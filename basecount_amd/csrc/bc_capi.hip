@@ -280,15 +280,19 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     const auto sp = h->n_reads ? host_spans(*h) : std::pair<int, int64_t>(0, 0);
     d->max_span = sp.first;
     d->max_end = sp.second;
+    if (h->seq_layout != BC_SEQ_BAM) return fail(BC_E_ARG, "bc_reads_upload: host batch must be BC_SEQ_BAM");
     const size_t n = (size_t)h->n_reads;
     void* p[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    const size_t sz[7] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4, (size_t)h->seq_bytes,
+    // the sequence buffer is sized for BC_SEQ_EVENT (converted in place after the copy)
+    const size_t sz[7] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4, bc::seq_event_bytes(h->seq_bytes),
                           h->qual ? (size_t)h->qual_bytes : 0};
+    const size_t cp[7] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6]};
     const void* src[7] = {h->pos, h->cig_beg, h->cig_n, h->seq_nib, h->cigar, h->seq, h->qual};
     for (int i = 0; i < 7; ++i) {
         if (!sz[i]) continue;
         hipError_t e = hipMalloc(&p[i], sz[i]);
-        if (e == hipSuccess) e = hipMemcpyAsync(p[i], src[i], sz[i], hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess && cp[i]) e = hipMemcpyAsync(p[i], src[i], cp[i], hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess && i == 5) e = bc::launch_seq_event(c->stream, (const uint8_t*)p[5], h->seq_bytes, (uint8_t*)p[5]);
         if (e != hipSuccess) {
             for (int j = 0; j <= i; ++j)
                 if (p[j]) (void)hipFree(p[j]);
@@ -302,6 +306,7 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     d->cigar = (const uint32_t*)p[4];
     d->seq = (const uint8_t*)p[5];
     d->qual = (const uint8_t*)p[6];
+    d->seq_layout = BC_SEQ_EVENT;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return BC_OK;
 }
@@ -325,7 +330,7 @@ int bc_count(bc_ctx* c, const bc_reads* r, int64_t ref_len, uint32_t mbq, int nc
     if (!d_hist && ref_len > 0) return fail(BC_E_ARG, "d_hist is NULL");
     if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
     DeviceGuard g(c->device);
-    if (r->sorted && r->max_span <= bc::kTileMaxSpan) {
+    if (r->sorted && r->max_span <= bc::kTileMaxSpan && r->seq_layout == BC_SEQ_EVENT && !((uintptr_t)r->seq & 15u)) {
         // sorted batch: the tiled kernel in accumulate mode (plain read-add-write per owned tile)
         Timed tm(c, BC_K_PILEUP);
         HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, ref_len, r->max_end, mbq, ncols, false, true, 0.0, 0.0,
@@ -347,6 +352,10 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
     if (r->max_span > bc::kTileMaxSpan)
         return fail(BC_E_ARG, "bc_pileup: max_span above 4096; use bc_count + bc_stats");
     if (mbq > 0 && r->n_reads > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+    if (r->n_reads > 0 && r->seq_layout != BC_SEQ_EVENT)
+        return fail(BC_E_ARG, "bc_pileup needs seq_layout == BC_SEQ_EVENT (see bc_seq_to_event)");
+    if (r->n_reads > 0 && ((uintptr_t)r->seq & 15u))
+        return fail(BC_E_ARG, "bc_pileup needs a 16-byte aligned sequence buffer");
     if (L > 0 && (!d_counts || !d_cov || !d_ent || !d_sec)) return fail(BC_E_ARG, "NULL output");
     DeviceGuard g(c->device);
     Timed tm(c, BC_K_PILEUP);
@@ -441,6 +450,16 @@ int bc_stats(bc_ctx* c, const int32_t* d_hist, int64_t L, int k, double nf, doub
 }
 
 size_t bc_summary_work_bytes(int64_t L) { return bc::summary_work_bytes(L); }
+
+size_t bc_seq_event_bytes(int64_t seq_bytes) { return bc::seq_event_bytes(seq_bytes); }
+
+int bc_seq_to_event(bc_ctx* c, const uint8_t* d_bam, int64_t seq_bytes, uint8_t* d_event) {
+    if (!c || !d_event || (seq_bytes > 0 && !d_bam)) return fail(BC_E_ARG, "NULL argument");
+    if (seq_bytes < 0) return fail(BC_E_ARG, "seq_bytes < 0");
+    DeviceGuard g(c->device);
+    HIP_TRY(bc::launch_seq_event(c->stream, d_bam, seq_bytes, d_event));
+    return BC_OK;
+}
 
 int bc_summary(bc_ctx* c, const int32_t* d_cov, const double* d_ent, int64_t L, void* d_work, double* d_out) {
     if (!c || !d_out || !d_work) return fail(BC_E_ARG, "NULL argument");

@@ -39,6 +39,8 @@ constexpr int kNpBuf = 8192;   // numpy's default ufunc buffer size (reduction c
 // launchers (bc_kernels.hip); all async on `s`, return hipError_t
 hipError_t launch_count(hipStream_t s, const bc_reads& r, int64_t ref_len, uint32_t mbq, int ncols,
                         int32_t* hist, int reads_per_block, unsigned long long* d_err);
+size_t seq_event_bytes(int64_t seq_bytes);
+hipError_t launch_seq_event(hipStream_t s, const uint8_t* src, int64_t nbytes, uint8_t* dst);
 hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span);
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2,
                         int32_t* cov, double* pc, double* ent, double* sec);

@@ -19,6 +19,10 @@ namespace {
 // Packed LUT, 4 bits per code, 0xF = not counted.
 constexpr unsigned long long kNibCol = 0x5FFFFFF3FFF2F10Full;
 __device__ __forceinline__ unsigned nib_col(unsigned nib) { return (unsigned)(kNibCol >> (nib * 4)) & 0xFu; }
+// BC_SEQ_EVENT class -> count column: A 1->0, C 2->1, G 4->2, T 8->3, N 3->5, else 0xF.
+constexpr unsigned long long kEvCol = 0xFFFFFFF3FFF2510Full;
+// BAM code -> BC_SEQ_EVENT class (A 1, C 2, G 4, T 8, N 15 -> 3, others 0).
+constexpr unsigned long long kNibClass = 0x3000000800040210ull;
 
 __device__ __forceinline__ int64_t uni64(int64_t v) {
     int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffff));
@@ -41,6 +45,7 @@ struct CountArgs {
     int rpb;        // reads per workgroup chunk
     int max_span;   // upper bound of any read's reference span
     int sorted;
+    int layout;     // BC_SEQ_BAM / BC_SEQ_EVENT
     int32_t* hist;  // [ncols][ref_len]
     unsigned long long* err;
 };
@@ -94,7 +99,10 @@ __device__ __forceinline__ bool walk_read(const CountArgs& A, int64_t i, unsigne
             if (typ == 1) {
                 const uint32_t ni = sn + qoff;
                 const unsigned byte = A.seq[ni >> 1];
-                col = nib_col((ni & 1u) ? (byte & 15u) : (byte >> 4));
+                if (A.layout == BC_SEQ_EVENT)
+                    col = (unsigned)(kEvCol >> (((byte >> ((ni & 1u) * 4)) & 15u) * 4)) & 0xFu;
+                else
+                    col = nib_col((ni & 1u) ? (byte & 15u) : (byte >> 4));
                 counted = col != 0xFu;
                 if (QUAL) counted = counted && (uint32_t)A.qual[ni] >= A.mbq;  // count.cpp:56
             }
@@ -189,6 +197,48 @@ __global__ void k_span(const uint32_t* cig_beg, const uint32_t* cig_n, const uin
         best = v > best ? v : best;
     }
     if ((threadIdx.x & 63) == 0) atomicMax(out, best);
+}
+
+// BAM-packed sequence -> BC_SEQ_EVENT (in place allowed: every thread reads its 16 bytes before
+// writing them).  Bytes in [nbytes, out_bytes) become zero padding.
+__device__ __forceinline__ uint32_t event_byte(uint32_t b) {
+    const uint32_t hi = (uint32_t)(kNibClass >> ((b >> 4) * 4)) & 15u;  // base 2m (BAM high nibble)
+    const uint32_t lo = (uint32_t)(kNibClass >> ((b & 15u) * 4)) & 15u; // base 2m+1
+    return hi | (lo << 4);
+}
+
+__global__ void k_seq_event(const uint8_t* src, int64_t nbytes, uint8_t* dst, int64_t out_bytes) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 16;
+    for (int64_t o = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; o < out_bytes; o += stride) {
+        uint32_t w[4];
+        if (o + 16 <= nbytes && ((uintptr_t)(src + o) & 15u) == 0) {
+            const uint4 v = *(const uint4*)(src + o);
+            w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+        } else {
+            for (int i = 0; i < 4; ++i) {
+                w[i] = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const int64_t at = o + 4 * i + b;
+                    if (at < nbytes) w[i] |= (uint32_t)src[at] << (8 * b);
+                }
+            }
+        }
+        uint32_t r[4];
+        for (int i = 0; i < 4; ++i) {
+            r[i] = 0;
+            for (int b = 0; b < 4; ++b) {
+                const int64_t at = o + 4 * i + b;
+                if (at < nbytes) r[i] |= event_byte((w[i] >> (8 * b)) & 0xFFu) << (8 * b);
+            }
+        }
+        if (o + 16 <= out_bytes && ((uintptr_t)(dst + o) & 15u) == 0) {
+            *(uint4*)(dst + o) = make_uint4(r[0], r[1], r[2], r[3]);
+        } else {
+            for (int i = 0; i < 4; ++i)
+                for (int b = 0; b < 4; ++b)
+                    if (o + 4 * i + b < out_bytes) dst[o + 4 * i + b] = (uint8_t)(r[i] >> (8 * b));
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------ kernel 2
@@ -548,6 +598,7 @@ hipError_t launch_count(hipStream_t s, const bc_reads& r, int64_t ref_len, uint3
     A.rpb = rpb;
     A.max_span = r.max_span;
     A.sorted = r.sorted;
+    A.layout = r.seq_layout;
     A.hist = hist;
     A.err = d_err;
     const int64_t nblk = (r.n_reads + rpb - 1) / rpb;
@@ -555,6 +606,18 @@ hipError_t launch_count(hipStream_t s, const bc_reads& r, int64_t ref_len, uint3
         hipLaunchKernelGGL(k_count<true>, dim3((unsigned)nblk), dim3(kCountThreads), 0, s, A);
     else
         hipLaunchKernelGGL(k_count<false>, dim3((unsigned)nblk), dim3(kCountThreads), 0, s, A);
+    return hipGetLastError();
+}
+
+size_t seq_event_bytes(int64_t seq_bytes) {
+    return (size_t)((seq_bytes > 0 ? seq_bytes : 0) + 15) / 16 * 16 + 16;
+}
+
+hipError_t launch_seq_event(hipStream_t s, const uint8_t* src, int64_t nbytes, uint8_t* dst) {
+    const int64_t out = (int64_t)seq_event_bytes(nbytes);
+    int64_t blocks = (out / 16 + 255) / 256;
+    if (blocks > 256 * 32) blocks = 256 * 32;
+    hipLaunchKernelGGL(k_seq_event, dim3((unsigned)blocks), dim3(256), 0, s, src, nbytes, dst, out);
     return hipGetLastError();
 }
 

@@ -1,18 +1,22 @@
 // bc_pileup.hip — the fused, position-tiled pileup kernel (kernel 1 + kernel 2 in ONE launch).
 //
-// Layout: the reference is cut into 64-position tiles; a tile is owned by a group of S waves
-// whose 64 lanes each OWN one reference position.  Reads are coordinate-sorted, so the reads
-// overlapping a tile form one contiguous index range, found in-kernel by a 64-ary search over
-// pos[].  Each read of that range is resolved once per tile: every lane looks up the read's
-// CIGAR at its own position (count.cpp:40-96) and adds the base / deletion it sees to a packed
-// register counter.  No atomics and no histogram memset: the S waves of a group are reduced
-// through LDS, the tile's counts are written once with coalesced stores (count.cpp's
-// baseCounts), and the per-position statistics of main.py:29-53 are computed in the same
-// launch (kernel 2 fused), the 2k fp64 terms of a tile spread over the group's lanes.
+// Layout: the reference is cut into 64-position tiles; a tile is owned by a group of S waves.
+// Reads are coordinate-sorted, so the reads overlapping a tile form one contiguous index range,
+// found in-kernel by a 64-ary search over pos[].  They are processed in chunks of 64: each lane
+// loads one read and decodes its CIGAR into a run table (count.cpp:40-96 semantics), the chunk's
+// packed sequence is staged into LDS, and then the chunk is walked with
+//     lane = (window g = lane >> 3, read slot s = lane & 7):
+// the lane assembles the 8 event classes its read has in reference window [t0+8g, t0+8g+8) as
+// ONE 32-bit word (a funnel shift of the BC_SEQ_EVENT sequence per CIGAR run, deletions as class
+// 1100) and counts all 8 positions x 6 columns with SWAR nibble counters: ~30 VALU per 8 bases.
+// No atomics and no histogram memset: the 8 read slots are reduced with DPP, the S waves of a
+// group through LDS, the tile's counts are written once with coalesced stores (count.cpp's
+// baseCounts), and the per-position statistics of main.py:29-53 are computed in the same launch
+// (kernel 2 fused).  Reads with more than 8 CIGAR ops / 4 runs take a per-position walk.
 //
-// Lanes at positions >= L (the last, partial tile and "edge" tiles past the reference end,
-// up to the furthest read end) do not count: a counted event there is the reference's
-// std::out_of_range (count.cpp:60-65,85) and is recorded as the first offending read index.
+// Positions >= L (the last, partial tile and "edge" tiles past the reference end, up to the
+// furthest read end) do not count: a counted event there is the reference's std::out_of_range
+// (count.cpp:60-65,85) and is recorded as the first offending read index.
 #include <cstring>
 
 #include "bc_internal.h"
@@ -21,13 +25,17 @@ namespace bc {
 namespace {
 
 constexpr int kTile = 64;
-// BAM 4-bit code -> count column (A0 C1 G2 T3 N5); 6 = not counted (junk field).
-// Same letter mapping as count.cpp:58-65 through pysam's "=ACMGRSVTWYHKDBN" decode.
-constexpr unsigned long long kNibCol6 = 0x5666666366626106ull;
+// BC_SEQ_EVENT class -> count column (A0 C1 G2 T3 N5); 6 = not counted (junk field).
+// The classes are count.cpp:58-65's letters through pysam's "=ACMGRSVTWYHKDBN" decode.
+constexpr unsigned long long kNibCol6 = 0x6666666366625106ull;
+constexpr uint32_t kM1 = 0x11111111u;   // bit 0 of every nibble
+constexpr uint32_t kClsDel = 0xCCCCCCCCu;  // class 1100 (deletion / ref-skip) in every nibble
 constexpr int kField = 10;  // packed counter: six 10-bit fields + junk at bit 60; flush < 1024
 constexpr int kJunk = 60;
 constexpr int kBatch = 8;   // reads whose sequence loads are in flight together
-constexpr int kPre = 8;     // CIGAR words preloaded per read (lane-parallel)
+constexpr int kPre = 8;     // CIGAR words decoded per read at chunk load (more -> complex path)
+constexpr int kStage = 5120;     // LDS bytes per wave for a chunk's sequence (64 reads x 150 bp)
+constexpr int kStageRegion = kStage + 32;  // + one 16-byte pad before and after
 constexpr uint32_t kNone = 0xFFFFFFFFu;  // packed event: none
 constexpr uint32_t kDel = 0x80000000u;   // packed event: deletion / ref-skip
 
@@ -59,62 +67,128 @@ struct PileArgs {
     double* ent;
     double* sec;
     unsigned long long* err;
+    int64_t seq_words;   // readable 32-bit words of seq (bc_seq_event_bytes / 4)
+    int64_t qual_bytes;
+    int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 8 no stats math,
+                 // 16 no stores, 32 no sequence staging
 };
 
-// First index i in [0, n) with pos[i] >= v (n if none), by one wave: 64 probes per round.
-__device__ __forceinline__ int64_t lower_bound64(const int32_t* pos, int64_t n, int64_t v, int lane) {
-    int64_t lo = 0, hi = n;  // answer in [lo, hi]
-    while (hi - lo > 64) {
-        const int64_t step = (hi - lo) / 65;
-        const int64_t idx = lo + (int64_t)(lane + 1) * (step > 0 ? step : 1);
-        const bool less = idx < hi && (int64_t)pos[idx] < v;
-        const unsigned long long m = __ballot(less);
-        const int c = __popcll(m);  // sorted: the lanes with pos < v are a prefix
-        const int64_t s = step > 0 ? step : 1;
-        const int64_t nlo = c ? lo + (int64_t)c * s + 1 : lo;
-        const int64_t nhi = (c < 64 && lo + (int64_t)(c + 1) * s < hi) ? lo + (int64_t)(c + 1) * s : hi;
-        lo = nlo;
-        hi = nhi;
-    }
-    const int64_t idx = lo + lane;
-    const bool less = idx < hi && (int64_t)pos[idx] < v;
-    return lo + __popcll(__ballot(less));
-}
-
-// Packed event of read r (its CIGAR in w[]) at event index j (lane position - start):
-// nibble index of the aligned base, kDel | 0 for a deletion / skip, kNone otherwise.  The op
-// loop is uniform; only ops overlapping the tile window [jlo, jlo + 63] do per-lane work.
-__device__ __forceinline__ uint32_t resolve(int j, int jlo, uint32_t cn, const uint32_t (&w)[kPre], uint32_t sn,
-                                            const uint32_t* cg) {
+// Packed event of a "complex" read (more than 8 CIGAR ops, more than 4 runs, or huge indels)
+// at event index j (lane position - start): nibble index of the aligned base, kDel for a deletion
+// / skip, kNone otherwise.  The op loop is uniform (scalar loads); only ops overlapping the tile
+// window [jlo, jlo + 63] do per-lane work.  Rare: typical reads take the run tables below.
+__device__ __forceinline__ uint32_t resolve_slow(int j, int jlo, uint32_t cn, uint32_t sn, const uint32_t* cg) {
     uint32_t e = kNone;
     const int jhi = jlo + kTile - 1;
     uint32_t rc = 0, qc = 0;
-    const uint32_t nk = cn < (uint32_t)kPre ? cn : (uint32_t)kPre;
-#pragma unroll
-    for (int k = 0; k < kPre; ++k) {
-        if ((uint32_t)k < nk) {
-            const uint32_t op = w[k] & 15u, len = w[k] >> 4;
-            if (mlike(op) || dlike(op)) {
-                if ((int)(rc + len) > jlo && (int)rc <= jhi) {
-                    const uint32_t d = (uint32_t)(j - (int)rc);
-                    if (d < len) e = mlike(op) ? sn + qc + d : kDel;
-                }
-                rc += len;
-            }
-            if (qcons(op)) qc += len;
-        }
-    }
-    for (uint32_t k = kPre; k < cn && (int)rc <= jhi; ++k) {  // long CIGARs: rest from memory
+    for (uint32_t k = 0; k < cn && (int)rc <= jhi; ++k) {
         const uint32_t wk = cg[k];
         const uint32_t op = wk & 15u, len = wk >> 4;
         if (mlike(op) || dlike(op)) {
-            const uint32_t d = (uint32_t)(j - (int)rc);
-            if (d < len) e = mlike(op) ? sn + qc + d : kDel;
+            if ((int)(rc + len) > jlo) {
+                const uint32_t d = (uint32_t)(j - (int)rc);
+                if (d < len) e = mlike(op) ? sn + qc + d : kDel;
+            }
             rc += len;
         }
         if (qcons(op)) qc += len;
     }
     return e;
+}
+
+// Run table of a read: its reference-consuming CIGAR ops as at most 4 runs, each packed as
+//   bits 0-12 start (reference offset from the read start), bit 13 deletion/skip,
+//   bits 16-31 signed query delta (query offset = event index + delta; M/=/X runs with the same
+//   delta merge, so S/H/P between them and the M/=/X distinction vanish).
+// count.cpp:40-96 semantics: M/=/X consume both, I the query only, D/N the reference only.
+constexpr uint32_t kRunDS = 1u << 13;
+constexpr int kMaxRuns = 4;
+
+struct RunTable {
+    uint32_t run[kMaxRuns];
+    uint32_t span;
+    uint32_t qlen;  // query bases consumed (M/=/X/I) by the decoded ops
+    int nrun;
+    bool complex;
+};
+
+__device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn) {
+    RunTable T;
+#pragma unroll
+    for (int i = 0; i < kMaxRuns; ++i) T.run[i] = 0;
+    T.nrun = 0;
+    T.complex = cn > (uint32_t)kPre;
+    uint32_t rc = 0, qc = 0;
+    int last = -1, lastqd = 0;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+        if ((uint32_t)k < cn) {
+            const uint32_t op = w[k] & 15u, len = w[k] >> 4;
+            uint32_t packed = 0;
+            bool add = false;
+            if (mlike(op)) {
+                const int qd = (int)qc - (int)rc;
+                if (!(last == 0 && lastqd == qd)) {
+                    add = true;
+                    packed = (rc & 0x1FFFu) | ((uint32_t)qd << 16);
+                    if (qd < -32768 || qd > 32767) T.complex = true;
+                }
+                last = 0;
+                lastqd = qd;
+                rc += len;
+                qc += len;
+            } else if (dlike(op)) {
+                if (last != 1) {
+                    add = true;
+                    packed = (rc & 0x1FFFu) | kRunDS;
+                }
+                last = 1;
+                rc += len;
+            } else if (op == 1) {
+                qc += len;
+            }
+            if (add) {
+                if (T.nrun >= kMaxRuns) T.complex = true;
+#pragma unroll
+                for (int i = 0; i < kMaxRuns; ++i)
+                    if (T.nrun == i) T.run[i] = packed;
+                ++T.nrun;
+            }
+        }
+    }
+    if (rc >= 0x1FFFu) T.complex = true;
+    T.span = rc;
+    T.qlen = qc;
+    return T;
+}
+
+// First indices with pos >= v_lo (lanes 0-31) and pos >= v_hi (lanes 32-63), searched together:
+// 32 probes per half-wave per round.  Returns {lower_bound(v_lo), lower_bound(v_hi)}.
+__device__ __forceinline__ void lower_bound_pair(const int32_t* pos, int64_t n, int64_t v_lo, int64_t v_hi, int lane,
+                                                 int64_t& r_lo, int64_t& r_hi) {
+    const int h = lane >> 5, l = lane & 31;
+    const int64_t v = h ? v_hi : v_lo;
+    int64_t lo = 0, hi = n;  // answer in [lo, hi] (per half)
+    while (__any(hi - lo > 32)) {
+        const bool act = hi - lo > 32;
+        const int64_t s = act ? ((hi - lo) / 33 > 0 ? (hi - lo) / 33 : 1) : 1;
+        const int64_t idx = lo + (int64_t)(l + 1) * s;
+        const bool less = act && idx < hi && (int64_t)pos[idx] < v;
+        const unsigned long long m = __ballot(less);
+        const int c = __popc(h ? (unsigned)(m >> 32) : (unsigned)m);
+        if (act) {
+            const int64_t nlo = c ? lo + (int64_t)c * s + 1 : lo;
+            const int64_t nhi = (c < 32 && lo + (int64_t)(c + 1) * s < hi) ? lo + (int64_t)(c + 1) * s : hi;
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    const int64_t idx = lo + l;
+    const bool less = idx < hi && (int64_t)pos[idx] < v;
+    const unsigned long long m = __ballot(less);
+    const int64_t res = lo + __popc(h ? (unsigned)(m >> 32) : (unsigned)m);
+    r_lo = __shfl(res, 0);
+    r_hi = __shfl(res, 32);
 }
 
 __device__ __forceinline__ void flush_acc(unsigned long long& acc, uint32_t (&cnt)[6]) {
@@ -134,8 +208,7 @@ __device__ __forceinline__ void count_event(uint32_t e, uint32_t byte, uint32_t 
         col = 4;
         ok = true;
     } else {
-        const unsigned nib = (e & 1u) ? (byte & 15u) : (byte >> 4);
-        col = nib_col6(nib);
+        col = nib_col6((byte >> ((e & 1u) * 4)) & 15u);
         ok = e != kNone && col != 6u;
         if (QUAL) ok = ok && qv >= mbq;
     }
@@ -146,111 +219,383 @@ __device__ __forceinline__ void count_event(uint32_t e, uint32_t byte, uint32_t 
     acc += 1ull << (ok ? col * kField : (unsigned)kJunk);
 }
 
-template <bool QUAL, int K, bool STATS>
-__global__ __launch_bounds__(1024) void k_pileup(PileArgs A) {
-    // reduction area: [16 waves][6][64] u32; reused as the stats terms [4 groups][12][64] f64
-    __shared__ __attribute__((aligned(16))) unsigned char smem[16 * 6 * kTile * 4];
-    __shared__ uint32_t fin[4][6][kTile];  // final counts of each group's tile
-    uint32_t* red = (uint32_t*)smem;
-    double* terms = (double*)smem;
+// Fused kernel 2, part 1: the fp64 terms -(p*log2(p)) of a tile's primary (c < K) and
+// secondary (K <= s < 2K) distributions, one per lane over the group (main.py:37-53), plus the
+// percentages.  Kept out of line: inlined, the log2 constants would be hoisted into registers
+// for the whole kernel and push the read walk into spills.
+template <int K>
+__device__ __attribute__((noinline)) void tile_terms(const PileArgs& A, const uint32_t* fin_g, double* terms_g,
+                                                     int64_t t0, int first, int stride) {
+    const int64_t L = A.L;
+    for (int slot = first; slot < 2 * K * kTile; slot += stride) {
+        const int sc = slot / kTile, p = slot % kTile;
+        const int64_t Pp = t0 + p;
+        if (Pp >= L) continue;
+        uint32_t c[6];
+        int64_t cov = 0;
+        int am = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            c[j] = fin_g[j * kTile + p];
+            cov += c[j];
+            if (c[j] > c[am]) am = j;  // np.argmax: first maximum
+        }
+        double term = 0.0;
+        if (sc < K) {
+            if (cov != 0) {
+                const double pj = (double)c[sc] / (double)cov;
+                if (A.pc) A.pc[(int64_t)sc * L + Pp] = 100.0 * pj;
+                if (c[sc] != 0) term = -(pj * log2(pj));
+            } else if (A.pc) {
+                A.pc[(int64_t)sc * L + Pp] = -1.0;
+            }
+        } else {
+            const int j = sc - K;
+            const int64_t cov2 = cov - c[am];
+            if (cov2 != 0 && j != am && c[j] != 0) {
+                const double q = (double)c[j] / (double)cov2;
+                term = -(q * log2(q));
+            }
+        }
+        terms_g[sc * kTile + p] = term;
+    }
+}
 
+// Complex chunks (a read with more than 8 CIGAR ops, more than 4 runs or huge indels): lanes own
+// positions, each read of the chunk is resolved at the lane's position by walking its CIGAR
+// from memory (records in LDS hold absolute sequence nibble indices), kBatch reads at a time.
+template <bool QUAL>
+__device__ __forceinline__ void walk_complex(const PileArgs& A, const uint4* rec, int nr, int64_t P, int64_t t0,
+                                             int64_t rbase, bool beyond, uint32_t mcn, uint32_t mcb,
+                                             unsigned long long& acc, int64_t& bad) {
+    const uint8_t* sp = A.seq ? A.seq : (const uint8_t*)A.pos;  // never dereferenced at a bad index
+    for (int r0 = 0; r0 < nr; r0 += kBatch) {
+        uint32_t e[kBatch];
+        for (int u = 0; u < kBatch; ++u) {
+            const int r = r0 + u;
+            uint32_t x = kNone;
+            if (r < nr) {
+                const uint4 a = rec[r * 2];
+                x = resolve_slow((int)(P - (int64_t)(int32_t)a.x), (int)(t0 - (int32_t)a.x), rdl(mcn, r), a.y,
+                                 A.cigar + rdl(mcb, r));
+            }
+#pragma unroll
+            for (int v = kBatch - 1; v > 0; --v) e[v] = e[v - 1];
+            e[0] = x;
+        }
+#pragma unroll
+        for (int u = 0; u < kBatch / 2; ++u) {  // e[kBatch-1-u] holds read r0+u
+            const uint32_t t = e[u];
+            e[u] = e[kBatch - 1 - u];
+            e[kBatch - 1 - u] = t;
+        }
+        uint32_t byte[kBatch], qv[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+            const uint32_t idx = e[u] < kDel ? e[u] : 0u;
+            byte[u] = (uint32_t)sp[idx >> 1];
+            qv[u] = QUAL ? (uint32_t)A.qual[idx] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u)
+            count_event<QUAL>(e[u], byte[u], qv[u], A.mbq, beyond, rbase + r0 + u, acc, bad);
+    }
+}
+
+// ---- SWAR counters of a lane's 8-position window ------------------------------------------
+// a4[c]: nibble k = count of column c at window position k; at most 15 reads are added before
+// the wave folds them into cnt[] (a sum over the 8 read slots is then <= 120: fits a byte).
+struct Swar {
+    uint32_t a4[6];
+};
+
+__device__ __forceinline__ uint32_t lo32_bit(int sh) { return (uint32_t)(1ull << sh); }  // sh in [0, 32]
+// nibbles [kl, kh) of a window word, 0 <= kl <= kh <= 8
+__device__ __forceinline__ uint32_t nib_range(int kl, int kh) { return lo32_bit(4 * kh) - lo32_bit(4 * kl); }
+
+template <int NC>
+__device__ __forceinline__ void swar_add(Swar& W, uint32_t x) {
+    const uint32_t x1 = x >> 1, x2 = x >> 2, x3 = x >> 3;
+    W.a4[0] += x & ~x1 & kM1;   // A  0001
+    W.a4[1] += x1 & ~x & kM1;   // C  0010
+    W.a4[2] += x2 & ~x3 & kM1;  // G  0100
+    W.a4[3] += x3 & ~x2 & kM1;  // T  1000
+    W.a4[4] += x2 & x3 & kM1;   // DS 1100
+    if (NC == 6) W.a4[5] += x & x1 & kM1;  // N 0011
+}
+
+// sum over the 8 read slots (lanes 8g .. 8g+7): quad xor 1, quad xor 2, half-row mirror
+__device__ __forceinline__ uint32_t sum8(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    return v;
+}
+
+// Fold the window counters into cnt[] of this lane's own position (8g + s == lane).  Must be
+// called by the whole wave.  Byte b of the even / odd half holds window position 2b / 2b + 1.
+template <int NC>
+__device__ __forceinline__ void swar_fold(Swar& W, uint32_t (&cnt)[6], int s8) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t b0 = sum8(W.a4[c] & 0x0F0F0F0Fu), b1 = sum8((W.a4[c] >> 4) & 0x0F0F0F0Fu);
+        cnt[c] += (((s8 & 1) ? b1 : b0) >> (8 * (s8 >> 1))) & 0xFFu;
+        W.a4[c] = 0;
+    }
+}
+
+// SWAR mask of 8 bases that pass the quality test, from their 8 quality bytes (q0: bases 0-3).
+__device__ __forceinline__ uint32_t ge_bytes(uint32_t q, uint32_t m) {  // per byte q >= m, m in [1, 255]
+    const uint32_t H = 0x80808080u;
+    const uint32_t t = (q | H) - (m & 0x7Fu) * 0x01010101u;  // high bit: low7(q) >= low7(m)
+    return (m & 0x80u) ? (q & t & H) : ((q | t) & H);
+}
+__device__ __forceinline__ uint32_t qual_nibmask(uint32_t q0, uint32_t q1, uint32_t m) {
+    if (m > 255u) return 0u;
+    uint32_t b0 = (ge_bytes(q0, m) >> 7) * 15u, b1 = (ge_bytes(q1, m) >> 7) * 15u;
+    b0 |= b0 >> 4;
+    b1 |= b1 >> 4;
+    return __builtin_amdgcn_perm(b1, b0, 0x06040200u);
+}
+
+// The 8 event classes at nibble indices n0 .. n0+7 of the sequence (unstaged: global memory).
+template <bool STAGED>
+__device__ __forceinline__ uint32_t fetch8(const PileArgs& A, const uint32_t* words, int64_t n0) {
+    if (STAGED) {
+        // staged words have one readable pad word before and after; windows that matter have
+        // n0 >= -7, anything else is masked off after the fetch
+        int w0 = (int)(n0 >> 3);
+        w0 = w0 < -1 ? -1 : (w0 > kStage / 4 ? kStage / 4 : w0);
+        return __builtin_amdgcn_alignbit(words[w0 + 1], words[w0], (uint32_t)(n0 & 7) * 4u);
+    }
+    const int64_t w0 = n0 >> 3, nw = A.seq_words;
+    const int64_t i0 = w0 < 0 ? 0 : (w0 >= nw ? nw - 1 : w0);
+    const int64_t i1 = w0 + 1 < 0 ? 0 : (w0 + 1 >= nw ? nw - 1 : w0 + 1);
+    const uint32_t lo = (w0 >= 0 && w0 < nw) ? words[i0] : 0u;
+    const uint32_t hi = (w0 + 1 >= 0 && w0 + 1 < nw) ? words[i1] : 0u;
+    uint32_t v = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(n0 & 7) * 4u);
+    return v;
+}
+
+// quality mask of bases n0 .. n0+7 (unstaged chunks only; staged ones are masked at staging)
+__device__ __forceinline__ uint32_t qual_mask_at(const PileArgs& A, int64_t n0) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int64_t i = n0 + k;
+        if (i >= 0 && i < A.qual_bytes && (uint32_t)A.qual[i] >= A.mbq) m |= 0xFu << (4 * k);
+    }
+    return m;
+}
+
+// Walk a chunk of nr reads (records in LDS, padded with empty records to 64) with lane = (window
+// g, read slot s): read it*8 + s in iteration it.  NR: the chunk's largest run count (1, 2, 4).
+template <int NR, bool STAGED, bool QUAL, int NC>
+__device__ __forceinline__ void walk_swar(const PileArgs& A, const uint4* rec, const uint32_t* words, int nr, int gb,
+                                          int s8, int64_t rbase, bool edge, uint32_t bmask, Swar& W, int& it4,
+                                          uint32_t (&cnt)[6], int64_t& bad) {
+    const int iters = (nr + 7) >> 3;
+    for (int it = 0; it < iters; ++it) {
+        const int r = it * 8 + s8;
+        const uint4 a = rec[r * 2];
+        uint4 b = make_uint4(0u, 0u, 0u, 0u);
+        if (NR > 1) b = rec[r * 2 + 1];
+        const int j0 = gb - (int)a.x;  // window start relative to the read start
+        const int span = (int)(a.z & 0xFFFFu);
+        const int nrun = (int)(a.z >> 16);
+        const uint32_t runs[4] = {a.w, b.x, b.y, b.z};
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const uint32_t wk = runs[k];
+            const int sk = (int)(wk & 0x1FFFu);
+            const int ek = (k + 1 < NR && k + 1 < nrun) ? (int)(runs[k + 1 < NR ? k + 1 : k] & 0x1FFFu) : span;
+            int kl = sk - j0;
+            kl = kl < 0 ? 0 : (kl > 8 ? 8 : kl);
+            int kh = ek - j0;
+            kh = kh < kl ? kl : (kh > 8 ? 8 : kh);
+            if (NR > 1 && k >= nrun) kh = kl;
+            const uint32_t m = nib_range(kl, kh);
+            const int64_t n0 = (int64_t)a.y + j0 + ((int32_t)wk >> 16);
+            uint32_t v = fetch8<STAGED>(A, words, n0);
+            if (QUAL && !STAGED) v &= qual_mask_at(A, n0);
+            v = (wk & kRunDS) ? kClsDel : v;
+            x |= v & m;
+        }
+        if (edge) {  // events at positions >= L: the reference's out_of_range
+            if ((x & bmask) && rbase + r < bad) bad = rbase + r;
+            x &= ~bmask;
+        }
+        swar_add<NC>(W, x);
+        if (++it4 == 15) {
+            swar_fold<NC>(W, cnt, s8);
+            it4 = 0;
+        }
+    }
+}
+
+constexpr int kFinBytes = 4 * 6 * kTile * 4;
+
+// dynamic LDS: [rec: nw x 2 KB][stage: nw x kStageRegion][fin: 6 KB][reduction / terms]
+__host__ __device__ inline size_t pileup_lds_bytes(int nw, int groups) {
+    const size_t red = (size_t)nw * 6 * kTile * 4, terms = (size_t)groups * 12 * kTile * 8;
+    return (size_t)nw * kTile * 2 * 16 + (size_t)nw * kStageRegion + kFinBytes + (red > terms ? red : terms);
+}
+
+template <bool QUAL, int K, bool STATS>
+__global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nw = blockDim.x >> 6;
     const int S = A.S;
     const int g = wave / S, ws = wave - g * S;
     const int groups = nw / S;
+    uint4* rec_all = (uint4*)dyn;
+    uint8_t* stage_all = dyn + (size_t)nw * kTile * 2 * 16;
+    uint32_t(*fin)[6][kTile] = (uint32_t(*)[6][kTile])(stage_all + (size_t)nw * kStageRegion);
+    uint32_t* red = (uint32_t*)((unsigned char*)fin + kFinBytes);
+    double* terms = (double*)red;
     const int64_t nblk_tiles = (A.n_tiles + groups - 1) / groups;
     const int64_t L = A.L;
+    const int s8 = lane & 7;
+    const bool qual_vec = ((uintptr_t)A.qual & 15u) == 0;
 
     for (int64_t bt = blockIdx.x; bt < nblk_tiles; bt += gridDim.x) {
         const int64_t t = bt * groups + g;
         const int64_t t0 = t * kTile;
         const int64_t P = t0 + lane;
+        const int gb = (int)t0 + 8 * (lane >> 3);  // this lane's window [gb, gb + 8)
         uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
         int64_t bad = INT64_MAX;
         if (t < A.n_tiles) {
-            const int64_t lo = lower_bound64(A.pos, A.n, t0 - A.max_span + 1, lane);
-            const int64_t hi = lower_bound64(A.pos, A.n, t0 + kTile, lane);
+            int64_t lo = 0, hi = 0;
+            if (!(A.ablate & 2)) lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
+            if (A.ablate & 1) hi = lo;
             const bool edge = t0 + kTile > L;  // uniform
             const bool beyond = P >= L;
+            uint32_t bmask = 0;                // window nibbles at positions >= L
+            if (edge) {
+                int64_t kL = L - gb;
+                kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
+                bmask = ~(lo32_bit(4 * (int)kL) - 1u);
+            }
             unsigned long long acc = 0;
             int pending = 0;
+            Swar W;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) W.a4[c] = 0;
+            int it4 = 0;
+            uint4* myrec = rec_all + wave * kTile * 2;
+            uint8_t* mystage = stage_all + (size_t)wave * kStageRegion + 16;
             for (int64_t base = lo + (int64_t)ws * 64; base < hi; base += (int64_t)S * 64) {
                 const int nr = (int)((hi - base) < 64 ? (hi - base) : 64);
-                uint32_t mpos = 0, mcn = 0, msn = 0, mcb = 0, mw[kPre];
+                // ---- chunk load: per-read fields lane-parallel, CIGAR -> run table (VALU)
+                RunTable T;
+                uint32_t mpos = 0, msn = 0, mcb = 0, mcn = 0;
+                T.nrun = 1;
+                T.complex = false;
+                T.span = 0;
+                T.qlen = 0;
 #pragma unroll
-                for (int i = 0; i < kPre; ++i) mw[i] = 0;
-                bool simple = true;
+                for (int i = 0; i < kMaxRuns; ++i) T.run[i] = 0;
                 if (lane < nr) {
                     const int64_t r = base + lane;
                     mpos = (uint32_t)A.pos[r];
                     mcb = A.cig_beg[r];
                     mcn = A.cig_n[r];
                     msn = A.seq_nib[r];
-                    mw[0] = mcn ? A.cigar[mcb] : 0u;
-                    simple = mcn == 1 && mlike(mw[0] & 15u);
-                }
-                const bool fast = __all(simple);  // every read of the chunk is one M/=/X op
-                if (!fast && lane < nr) {
+                    uint32_t w[kPre];
 #pragma unroll
-                    for (int i = 1; i < kPre; ++i)
-                        if ((uint32_t)i < mcn) mw[i] = A.cigar[mcb + i];
+                    for (int i = 0; i < kPre; ++i) w[i] = (uint32_t)i < mcn ? A.cigar[mcb + i] : 0u;
+                    T = decode_runs(w, mcn);
+                    if (T.nrun == 0) {  // no reference-consuming op: never counts
+                        T.nrun = 1;
+                        T.run[0] = 0;
+                        T.span = 0;
+                    }
                 }
-                if (pending + nr >= (1 << kField) - 1) {
-                    flush_acc(acc, cnt);
-                    pending = 0;
+                const bool cx = __any(T.complex);
+                int maxrun = T.nrun;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const int v2 = __shfl_xor(maxrun, o);
+                    maxrun = v2 > maxrun ? v2 : maxrun;
                 }
-                pending += nr;
-                for (int r0 = 0; r0 < nr; r0 += kBatch) {
-                    uint32_t e[kBatch];
-                    if (fast) {
-#pragma unroll
-                        for (int u = 0; u < kBatch; ++u) {
-                            e[u] = kNone;
-                            if (r0 + u < nr) {
-                                const uint32_t j = (uint32_t)(P - (int64_t)(int32_t)rdl(mpos, r0 + u));
-                                if (j < (rdl(mw[0], r0 + u) >> 4)) e[u] = rdl(msn, r0 + u) + j;
+                maxrun = __builtin_amdgcn_readfirstlane(maxrun);
+                // ---- stage the chunk's sequence (BC_SEQ_EVENT words) into LDS; with a quality
+                // threshold, bases below it are cleared here (count.cpp:56)
+                uint32_t blo = 0xFFFFFFFFu, bhi = 0;
+                if (lane < nr && T.qlen) {
+                    blo = msn >> 1;
+                    bhi = (msn + T.qlen + 1) >> 1;
+                }
+                for (int o = 32; o > 0; o >>= 1) {
+                    const uint32_t l2 = __shfl_xor(blo, o), h2 = __shfl_xor(bhi, o);
+                    blo = l2 < blo ? l2 : blo;
+                    bhi = h2 > bhi ? h2 : bhi;
+                }
+                uint32_t seg_lo = __builtin_amdgcn_readfirstlane(blo);
+                const uint32_t seg_hi = __builtin_amdgcn_readfirstlane(bhi);
+                seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
+                const bool staged = !cx && seg_hi - seg_lo <= (uint32_t)kStage && !(A.ablate & 32);
+                if (staged) {
+                    for (uint32_t off = lane * 16u; off < seg_hi - seg_lo; off += 1024u) {
+                        uint4 v = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
+                        if (QUAL) {
+                            const int64_t q0 = 2 * ((int64_t)seg_lo + off);  // first base of the piece
+                            uint32_t qw[8];
+                            if (qual_vec && q0 + 32 <= A.qual_bytes) {
+                                const uint4 qa = *(const uint4*)(A.qual + q0), qb = *(const uint4*)(A.qual + q0 + 16);
+                                qw[0] = qa.x, qw[1] = qa.y, qw[2] = qa.z, qw[3] = qa.w;
+                                qw[4] = qb.x, qw[5] = qb.y, qw[6] = qb.z, qw[7] = qb.w;
+                            } else {
+                                for (int i = 0; i < 8; ++i) {
+                                    qw[i] = 0;
+                                    for (int bb = 0; bb < 4; ++bb) {
+                                        const int64_t at = q0 + 4 * i + bb;
+                                        if (at < A.qual_bytes) qw[i] |= (uint32_t)A.qual[at] << (8 * bb);
+                                    }
+                                }
                             }
+                            v.x &= qual_nibmask(qw[0], qw[1], A.mbq);
+                            v.y &= qual_nibmask(qw[2], qw[3], A.mbq);
+                            v.z &= qual_nibmask(qw[4], qw[5], A.mbq);
+                            v.w &= qual_nibmask(qw[6], qw[7], A.mbq);
                         }
+                        *(uint4*)(mystage + off) = v;
+                    }
+                }
+                const uint32_t qbase = staged ? 2u * seg_lo : 0u;
+                myrec[lane * 2] = make_uint4(mpos, msn - qbase, T.span | ((uint32_t)T.nrun << 16), T.run[0]);
+                myrec[lane * 2 + 1] = make_uint4(T.run[1], T.run[2], T.run[3], 0u);
+                __builtin_amdgcn_wave_barrier();
+                const int64_t rbase = base;
+                if (cx) {
+                    if (pending + nr >= (1 << kField) - 1) {
+                        flush_acc(acc, cnt);
+                        pending = 0;
+                    }
+                    pending += nr;
+                    walk_complex<QUAL>(A, myrec, nr, P, t0, rbase, edge && beyond, mcn, mcb, acc, bad);
+                } else {
+                    const uint32_t* words = staged ? (const uint32_t*)mystage : (const uint32_t*)A.seq;
+#define BC_WALK(NR, ST)                                                                                     \
+    walk_swar<NR, ST, QUAL, K>(A, myrec, words, nr, gb, s8, rbase, edge, bmask, W, it4, cnt, bad)
+                    if (staged) {
+                        if (maxrun == 1) BC_WALK(1, true);
+                        else if (maxrun == 2) BC_WALK(2, true);
+                        else BC_WALK(4, true);
                     } else {
-                        // rolled resolver; results shift through e[] (one code copy, 8 moves)
-#pragma unroll
-                        for (int u = 0; u < kBatch; ++u) e[u] = kNone;
-                        for (int u = 0; u < kBatch; ++u) {
-                            uint32_t x = kNone;
-                            const int r = r0 + u;
-                            if (r < nr) {
-                                const int p0 = (int)rdl(mpos, r);
-                                uint32_t w[kPre];
-#pragma unroll
-                                for (int i = 0; i < kPre; ++i) w[i] = rdl(mw[i], r);
-                                x = resolve((int)(P - p0), (int)(t0 - p0), rdl(mcn, r), w, rdl(msn, r),
-                                            A.cigar + rdl(mcb, r));
-                            }
-#pragma unroll
-                            for (int v = kBatch - 1; v > 0; --v) e[v] = e[v - 1];
-                            e[0] = x;  // after the loop e[kBatch-1-u] holds read r0+u
-                        }
+                        if (maxrun == 1) BC_WALK(1, false);
+                        else if (maxrun == 2) BC_WALK(2, false);
+                        else BC_WALK(4, false);
                     }
-                    uint32_t byte[kBatch], qv[kBatch];
-#pragma unroll
-                    for (int u = 0; u < kBatch; ++u) {
-                        byte[u] = 0;
-                        qv[u] = 0;
-                        if (e[u] < kDel) {
-                            byte[u] = A.seq[e[u] >> 1];
-                            if (QUAL) qv[u] = A.qual[e[u]];
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < kBatch; ++u) {
-                        const int r = fast ? r0 + u : r0 + (kBatch - 1 - u);
-                        count_event<QUAL>(e[u], byte[u], qv[u], A.mbq, edge && beyond, base + r, acc, bad);
-                    }
+#undef BC_WALK
                 }
+                __builtin_amdgcn_wave_barrier();
             }
             flush_acc(acc, cnt);
+            if (it4) swar_fold<K>(W, cnt, s8);
             if (edge) {  // first offending read of this tile (std::out_of_range in the reference)
                 for (int o = 32; o > 0; o >>= 1) {
                     const int64_t b2 = __shfl_down(bad, o);
@@ -270,7 +615,7 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A) {
                     for (int c = 0; c < K; ++c) cnt[c] += red[(w2 * K + c) * kTile + lane];
                 }
         }
-        const bool own = t < A.n_tiles && t0 < L;  // tile holds real positions
+        const bool own = t < A.n_tiles && t0 < L && !(A.ablate & 16);  // tile holds real positions
         if (ws == 0) {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -282,48 +627,13 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A) {
                 fin[g][c][lane] = cnt[c];
             }
         }
-        if (!STATS) {
+        if (!STATS || (A.ablate & 8)) {
             if (S > 1) __syncthreads();
             continue;
         }
         __syncthreads();
-        // ---- fused kernel 2: terms p*log2(p) of the primary (c < K) and secondary (K <= s < 2K)
-        //      distributions, one per lane over the group, then ordered sums per position
-        //      (main.py:37-53; CPython sums left to right from int 0)
-        if (own) {
-            for (int slot = ws * 64 + lane; slot < 2 * K * kTile; slot += S * 64) {
-                const int sc = slot / kTile, p = slot % kTile;
-                const int64_t Pp = t0 + p;
-                if (Pp >= L) continue;
-                uint32_t c[6];
-                int64_t cov = 0;
-                int am = 0;
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    c[j] = fin[g][j][p];
-                    cov += c[j];
-                    if (c[j] > c[am]) am = j;  // np.argmax: first maximum
-                }
-                double term = 0.0;
-                if (sc < K) {
-                    if (cov != 0) {
-                        const double pj = (double)c[sc] / (double)cov;
-                        if (A.pc) A.pc[(int64_t)sc * L + Pp] = 100.0 * pj;
-                        if (c[sc] != 0) term = -(pj * log2(pj));
-                    } else if (A.pc) {
-                        A.pc[(int64_t)sc * L + Pp] = -1.0;
-                    }
-                } else {
-                    const int j = sc - K;
-                    const int64_t cov2 = cov - c[am];
-                    if (cov2 != 0 && j != am && c[j] != 0) {
-                        const double q = (double)c[j] / (double)cov2;
-                        term = -(q * log2(q));
-                    }
-                }
-                terms[(g * 2 * K + sc) * kTile + p] = term;
-            }
-        }
+        // ---- fused kernel 2: per-lane fp64 terms, then ordered sums per position
+        if (own) tile_terms<K>(A, &fin[g][0][0], terms + g * 2 * K * kTile, t0, ws * 64 + lane, S * 64);
         __syncthreads();
         if (own && ws == 0 && P < L) {
             int64_t cov = 0;
@@ -372,6 +682,8 @@ PileArgs make_args(const bc_reads& r, int64_t L, uint32_t mbq) {
     A.L = L;
     A.max_span = r.max_span;
     A.mbq = mbq;
+    A.seq_words = (int64_t)(seq_event_bytes(r.seq_bytes) / 4);
+    A.qual_bytes = r.qual ? r.qual_bytes : 0;
     return A;
 }
 
@@ -393,11 +705,13 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
     A.ent = ent;
     A.sec = sec;
     A.err = d_err;
+    if (const char* ab = std::getenv("BC_ABLATE")) A.ablate = std::atoi(ab);
     // waves per tile from the mean number of reads a tile walks
-    const double per_tile = L > 0 ? (double)r.n_reads * (double)(r.max_span + kTile) / (double)(kTile * (L + 1)) : 0.0;
+    // reads overlapping a tile ~ density * (span + 63); aim for ~48 reads per wave
+    const double per_tile = reach > 0 ? (double)r.n_reads * (double)(r.max_span + kTile - 1) / (double)reach : 0.0;
     int S = 1;
-    while (S < 16 && per_tile > 48.0 * S) S *= 2;
-    if (const char* e = std::getenv("BC_TILE_WAVES")) S = std::max(1, std::min(16, std::atoi(e)));
+    while (S < 8 && per_tile > 48.0 * S) S *= 2;
+    if (const char* e = std::getenv("BC_TILE_WAVES")) S = std::max(1, std::min(8, std::atoi(e)));
     A.S = S;
     const int nw = S >= 4 ? S : 4;
     const int groups = nw / S;
@@ -405,7 +719,18 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
     const int64_t cap = 256 * 64;
     if (blocks > cap) blocks = cap;
     const dim3 grid((unsigned)blocks), block(64 * nw);
-#define BC_PILE(Q, KK, ST) hipLaunchKernelGGL((k_pileup<Q, KK, ST>), grid, block, 0, s, A)
+    const size_t lds = pileup_lds_bytes(nw, groups);
+    // > 64 KiB of dynamic LDS must be allowed per kernel (160 KiB per CU on gfx950)
+#define BC_PILE(Q, KK, ST)                                                                                   \
+    do {                                                                                                     \
+        static bool attr_set = false;                                                                        \
+        if (!attr_set) {                                                                                     \
+            (void)hipFuncSetAttribute((const void*)k_pileup<Q, KK, ST>,                                      \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);               \
+            attr_set = true;                                                                                 \
+        }                                                                                                    \
+        hipLaunchKernelGGL((k_pileup<Q, KK, ST>), grid, block, lds, s, A);                                   \
+    } while (0)
     if (mbq > 0) {
         if (k == 5) {
             if (stats) BC_PILE(true, 5, true); else BC_PILE(true, 5, false);

@@ -15,6 +15,7 @@ import numpy as np
 from ._native import _libs, _load
 
 BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV = -1, -2, -3, -4
+BC_SEQ_BAM, BC_SEQ_EVENT = 0, 1
 KERNEL_NAMES = ("count", "stats", "reserved", "pileup", "summary", "amplicons")  # BC_K_* ids
 KERNEL_IDS = len(KERNEL_NAMES)
 
@@ -35,6 +36,8 @@ class BcReads(C.Structure):
         ("sorted", C.c_int32),
         ("max_span", C.c_int32),
         ("max_end", C.c_int64),
+        ("seq_layout", C.c_int32),  # BC_SEQ_BAM 0 / BC_SEQ_EVENT 1
+        ("reserved", C.c_int32),
     ]
 
 
@@ -69,6 +72,8 @@ def lib() -> C.CDLL:
         "bc_range_error": ([vp, C.POINTER(i64)], C.c_int),
         "bc_stats": ([vp, vp, i64, C.c_int, dbl, dbl, vp, vp, vp, vp], C.c_int),
         "bc_summary_work_bytes": ([i64], C.c_size_t),
+        "bc_seq_event_bytes": ([i64], C.c_size_t),
+        "bc_seq_to_event": ([vp, vp, i64, vp], C.c_int),
         "bc_summary": ([vp, vp, vp, i64, vp, vp], C.c_int),
         "bc_amplicons": ([vp, vp, vp, vp, i64, vp, vp, C.c_int32, vp], C.c_int),
         "bc_bcount_host": ([C.c_int, i64, u32, C.POINTER(BcReads), vp, C.POINTER(i64),
@@ -247,6 +252,11 @@ class Context:
         check(lib().bc_timing_report(self.h, n.ctypes.data, us.ctypes.data))
         return {name: (int(n[i]), float(us[i])) for i, name in enumerate(KERNEL_NAMES) if n[i]}
 
+    def seq_to_event(self, d_bam: int, seq_bytes: int, d_event: int) -> None:
+        """BAM-packed sequence -> BC_SEQ_EVENT (d_event may alias d_bam; it needs
+        seq_event_bytes(seq_bytes) bytes)."""
+        check(lib().bc_seq_to_event(self.h, d_bam, int(seq_bytes), d_event))
+
     def range_error(self) -> int:
         v = C.c_int64(-1)
         check(lib().bc_range_error(self.h, C.byref(v)))
@@ -278,6 +288,10 @@ class Graph:
                 self.h = None
         except Exception:
             pass
+
+
+def seq_event_bytes(seq_bytes: int) -> int:
+    return int(lib().bc_seq_event_bytes(int(seq_bytes)))
 
 
 def summary_work_bytes(L: int) -> int:

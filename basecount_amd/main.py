@@ -332,7 +332,9 @@ class _FileOnDevice:
         span = csum[f.cig_off[1:].astype(np.int64)] - csum[f.cig_off[:-1].astype(np.int64)]
         self.span = np.where(faulty, 0, span[sel.rec]) if sel.rec.size else np.zeros(0, np.int64)
         self.d_cigar = ctx.alloc(max(4, f.cigar.nbytes)).upload(f.cigar)
-        self.d_seq = ctx.alloc(max(4, f.seq.nbytes)).upload(f.seq)
+        # packed SEQ in the kernels' layout (BC_SEQ_EVENT), converted in place on the device
+        self.d_seq = ctx.alloc(D.seq_event_bytes(f.seq.nbytes)).upload(f.seq)
+        ctx.seq_to_event(self.d_seq.ptr, f.seq.nbytes, self.d_seq.ptr)
         self.d_qual = ctx.alloc(max(4, f.qual.nbytes)).upload(f.qual) if need_qual else None
         self.n_cig, self.n_seq, self.n_qual = f.cigar.size, f.seq.size, f.qual.size
         m = sel.pos.size
@@ -353,6 +355,7 @@ class _FileOnDevice:
         r.n_cigar_words = self.n_cig
         r.seq = self.d_seq.ptr
         r.seq_bytes = self.n_seq
+        r.seq_layout = D.BC_SEQ_EVENT
         if self.d_qual is not None:
             r.qual = self.d_qual.ptr
             r.qual_bytes = self.n_qual

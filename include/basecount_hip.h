@@ -41,14 +41,25 @@ extern "C" {
 #define BC_E_RANGE (-3) /* a counted event fell outside [0, refLen) (count.cpp:60-65,85 .at())   */
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
 
-#define BC_ABI_VERSION 1
+#define BC_ABI_VERSION 2
+
+/* Layouts of bc_reads.seq.
+ *   BC_SEQ_BAM   BAM packing: "=ACMGRSVTWYHKDBN" codes, two per byte, high nibble first
+ *                (what the host decoder produces; bc_reads_upload/bc_bcount_host inputs).
+ *   BC_SEQ_EVENT the device layout of the tiled kernel: one nibble per base in LINEAR order
+ *                (base i at bits 4*(i%8) of little-endian 32-bit word i/8), pre-classified to
+ *                event classes  A 0001, C 0010, G 0100, T 1000, N 0011, not counted 0000
+ *                (count.cpp:58-65 through pysam's decode: '=' and IUPAC codes count nowhere).
+ *                The buffer must hold bc_seq_event_bytes(seq_bytes) bytes (zero padding).
+ * bc_reads_upload produces BC_SEQ_EVENT; bc_seq_to_event converts a device buffer in place. */
+#define BC_SEQ_BAM 0
+#define BC_SEQ_EVENT 1
 
 /* A batch of pre-decoded, accepted reads of ONE reference, struct-of-arrays.
  * For read i (all fields as the reference's bcount sees them, count.cpp:22-38):
  *   starts[i]  = pos[i]                              (0-based reference_start)
  *   ctuples[i] = cigar[cig_beg[i] .. cig_beg[i]+cig_n[i])   BAM words: len << 4 | op
- *   reads[i][j]     = SEQ nibble at index seq_nib[i] + j    ("=ACMGRSVTWYHKDBN" codes, packed
- *                                                            two per byte, high nibble first)
+ *   reads[i][j]     = SEQ nibble at index seq_nib[i] + j    (layout: seq_layout, BC_SEQ_*)
  *   qualities[i][j] = qual[seq_nib[i] + j]                  (qual is indexed by nibble index)
  * i.e. seq_nib already includes the query_alignment_start (soft-clip) offset.
  * The same struct describes host arrays (bc_reads_upload input, bc_bcount_host) and device
@@ -68,6 +79,8 @@ typedef struct bc_reads {
     int32_t sorted;           /* 1 if pos[] is non-decreasing (enables the tiled kernel)       */
     int32_t max_span;         /* upper bound of every read's reference span (M/D/N/=/X bases)  */
     int64_t max_end;          /* upper bound of pos[i] + span[i] over the batch                */
+    int32_t seq_layout;       /* BC_SEQ_BAM or BC_SEQ_EVENT                                    */
+    int32_t reserved;         /* 0                                                             */
 } bc_reads;
 
 typedef struct bc_ctx bc_ctx;
@@ -90,8 +103,15 @@ int bc_memcpy_h2d(bc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);  /
 int bc_memcpy_d2h(bc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);  /* async */
 int bc_memset(bc_ctx* ctx, void* d_dst, int value, size_t bytes);              /* async */
 
-/* Copy a host batch to HBM (library-owned).  `sorted` and `max_span` of the device batch are
- * derived from the data (the host's values are ignored).  For batches assembled directly in
+/* Bytes a BC_SEQ_EVENT buffer needs for seq_bytes bytes of packed sequence. */
+size_t bc_seq_event_bytes(int64_t seq_bytes);
+/* Convert BAM-packed sequence (device) to BC_SEQ_EVENT: d_event (bc_seq_event_bytes bytes) may
+ * alias d_bam.  Async on the context's stream.                                                */
+int bc_seq_to_event(bc_ctx* ctx, const uint8_t* d_bam, int64_t seq_bytes, uint8_t* d_event);
+
+/* Copy a host batch (BC_SEQ_BAM) to HBM (library-owned, converted to BC_SEQ_EVENT).  `sorted`,
+ * `max_span` and `max_end` of the device batch are derived from the data (the host's values
+ * are ignored).  For batches assembled directly in
  * device memory the caller must set both truthfully: the tiled kernel trusts them.           */
 int bc_reads_upload(bc_ctx* ctx, const bc_reads* h_reads, bc_reads* d_reads);
 int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
@@ -110,7 +130,8 @@ int bc_count(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min
 /* Fused kernel 1 + kernel 2 — the hot path in ONE launch.  For a coordinate-sorted batch
  * (d_reads->sorted == 1, max_span <= 4096, max_end truthful) the reference is cut into
  * 64-position tiles; each tile finds its reads by a search over pos[], walks them with lanes
- * owning positions and register counters (no atomics, no histogram memset), and writes
+ * owning 8-position windows and SWAR register counters (no atomics, no histogram memset;
+ * needs seq_layout == BC_SEQ_EVENT), and writes
  *   d_counts [k][L] int32 (the reference's baseCounts columns, N only when k == 6),
  *   d_cov, d_pc (may be NULL), d_ent, d_sec  exactly as bc_stats defines them.
  * Out-of-range counted events are recorded for bc_range_error() as with bc_count.

@@ -19,6 +19,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 1200 python -m pytest tests -m gpu -x -q -s ${PYTEST_ARGS} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS} ;;
+    bench3) run bench3 600 python bench.py --config c3 --no-cpu-baseline ${BENCH_ARGS} ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --steps 200 ${BENCH_ARGS} ;;
   esac

@@ -34,7 +34,7 @@ constexpr int kField = 10;  // packed counter: six 10-bit fields + junk at bit 6
 constexpr int kJunk = 60;
 constexpr int kBatch = 8;   // reads whose sequence loads are in flight together
 constexpr int kPre = 8;     // CIGAR words decoded per read at chunk load (more -> complex path)
-constexpr int kStage = 5120;     // LDS bytes per wave for a chunk's sequence (64 reads x 150 bp)
+constexpr int kStage = 6144;     // LDS bytes per wave for a chunk's sequence (64 reads x <= 190 bp)
 constexpr int kStageRegion = kStage + 32;  // + one 16-byte pad before and after
 constexpr uint32_t kNone = 0xFFFFFFFFu;  // packed event: none
 constexpr uint32_t kDel = 0x80000000u;   // packed event: deletion / ref-skip
@@ -69,8 +69,8 @@ struct PileArgs {
     unsigned long long* err;
     int64_t seq_words;   // readable 32-bit words of seq (bc_seq_event_bytes / 4)
     int64_t qual_bytes;
-    int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 8 no stats math,
-                 // 16 no stores, 32 no sequence staging
+    int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 4 no walk, 8 no stats
+                 // math, 16 no stores, 32 no sequence staging
 };
 
 // Packed event of a "complex" read (more than 8 CIGAR ops, more than 4 runs, or huge indels)
@@ -96,63 +96,59 @@ __device__ __forceinline__ uint32_t resolve_slow(int j, int jlo, uint32_t cn, ui
     return e;
 }
 
-// Run table of a read: its reference-consuming CIGAR ops as at most 4 runs, each packed as
-//   bits 0-12 start (reference offset from the read start), bit 13 deletion/skip,
-//   bits 16-31 signed query delta (query offset = event index + delta; M/=/X runs with the same
-//   delta merge, so S/H/P between them and the M/=/X distinction vanish).
+// Run table of a read: its aligned (M/=/X) bases as at most 4 runs [st, en) of reference
+// offsets from the read start, each with a query delta qd (query offset = reference offset +
+// qd; consecutive M/=/X ops with the same delta merge, so the M/=/X distinction and S/H/P
+// between them vanish).  Every other reference offset in [0, span) is a deletion / ref-skip.
 // count.cpp:40-96 semantics: M/=/X consume both, I the query only, D/N the reference only.
-constexpr uint32_t kRunDS = 1u << 13;
 constexpr int kMaxRuns = 4;
 
 struct RunTable {
-    uint32_t run[kMaxRuns];
+    uint32_t st[kMaxRuns], en[kMaxRuns];
+    int32_t qd[kMaxRuns];
     uint32_t span;
     uint32_t qlen;  // query bases consumed (M/=/X/I) by the decoded ops
     int nrun;
+    bool gap;       // some reference offset in [0, span) is a deletion / ref-skip
     bool complex;
 };
 
 __device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn) {
     RunTable T;
 #pragma unroll
-    for (int i = 0; i < kMaxRuns; ++i) T.run[i] = 0;
+    for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
     T.nrun = 0;
+    T.gap = false;
     T.complex = cn > (uint32_t)kPre;
-    uint32_t rc = 0, qc = 0;
-    int last = -1, lastqd = 0;
+    uint32_t rc = 0, qc = 0, last_en = 0xFFFFFFFFu;
+    int last_qd = 0;
 #pragma unroll
     for (int k = 0; k < kPre; ++k) {
         if ((uint32_t)k < cn) {
             const uint32_t op = w[k] & 15u, len = w[k] >> 4;
-            uint32_t packed = 0;
-            bool add = false;
-            if (mlike(op)) {
+            if (mlike(op) && len) {
                 const int qd = (int)qc - (int)rc;
-                if (!(last == 0 && lastqd == qd)) {
-                    add = true;
-                    packed = (rc & 0x1FFFu) | ((uint32_t)qd << 16);
-                    if (qd < -32768 || qd > 32767) T.complex = true;
+                if (qd < -32768 || qd > 32767) T.complex = true;
+                if (last_en == rc && last_qd == qd) {  // extends the previous run
+#pragma unroll
+                    for (int i = 0; i < kMaxRuns; ++i)
+                        if (T.nrun - 1 == i) T.en[i] = rc + len;
+                } else {
+                    if (T.nrun >= kMaxRuns) T.complex = true;
+#pragma unroll
+                    for (int i = 0; i < kMaxRuns; ++i)
+                        if (T.nrun == i) T.st[i] = rc, T.en[i] = rc + len, T.qd[i] = qd;
+                    ++T.nrun;
                 }
-                last = 0;
-                lastqd = qd;
                 rc += len;
                 qc += len;
-            } else if (dlike(op)) {
-                if (last != 1) {
-                    add = true;
-                    packed = (rc & 0x1FFFu) | kRunDS;
-                }
-                last = 1;
+                last_en = rc;
+                last_qd = qd;
+            } else if (dlike(op) && len) {
+                T.gap = true;
                 rc += len;
             } else if (op == 1) {
                 qc += len;
-            }
-            if (add) {
-                if (T.nrun >= kMaxRuns) T.complex = true;
-#pragma unroll
-                for (int i = 0; i < kMaxRuns; ++i)
-                    if (T.nrun == i) T.run[i] = packed;
-                ++T.nrun;
             }
         }
     }
@@ -187,8 +183,12 @@ __device__ __forceinline__ void lower_bound_pair(const int32_t* pos, int64_t n, 
     const bool less = idx < hi && (int64_t)pos[idx] < v;
     const unsigned long long m = __ballot(less);
     const int64_t res = lo + __popc(h ? (unsigned)(m >> 32) : (unsigned)m);
-    r_lo = __shfl(res, 0);
-    r_hi = __shfl(res, 32);
+    // wave-uniform results (SGPRs): the chunk loops over [r_lo, r_hi) stay scalar
+    const uint32_t rl = (uint32_t)res, rh = (uint32_t)((uint64_t)res >> 32);
+    r_lo = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rh, 0) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)rl, 0));
+    r_hi = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rh, 32) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)rl, 32));
 }
 
 __device__ __forceinline__ void flush_acc(unsigned long long& acc, uint32_t (&cnt)[6]) {
@@ -275,7 +275,7 @@ __device__ __forceinline__ void walk_complex(const PileArgs& A, const uint4* rec
             const int r = r0 + u;
             uint32_t x = kNone;
             if (r < nr) {
-                const uint4 a = rec[r * 2];
+                const uint4 a = rec[r * 3];
                 x = resolve_slow((int)(P - (int64_t)(int32_t)a.x), (int)(t0 - (int32_t)a.x), rdl(mcn, r), a.y,
                                  A.cigar + rdl(mcb, r));
             }
@@ -364,9 +364,10 @@ __device__ __forceinline__ uint32_t fetch8(const PileArgs& A, const uint32_t* wo
     if (STAGED) {
         // staged words have one readable pad word before and after; windows that matter have
         // n0 >= -7, anything else is masked off after the fetch
-        int w0 = (int)(n0 >> 3);
+        const int n = (int)n0;
+        int w0 = n >> 3;
         w0 = w0 < -1 ? -1 : (w0 > kStage / 4 ? kStage / 4 : w0);
-        return __builtin_amdgcn_alignbit(words[w0 + 1], words[w0], (uint32_t)(n0 & 7) * 4u);
+        return __builtin_amdgcn_alignbit(words[w0 + 1], words[w0], (uint32_t)n << 2);
     }
     const int64_t w0 = n0 >> 3, nw = A.seq_words;
     const int64_t i0 = w0 < 0 ? 0 : (w0 >= nw ? nw - 1 : w0);
@@ -388,46 +389,73 @@ __device__ __forceinline__ uint32_t qual_mask_at(const PileArgs& A, int64_t n0) 
     return m;
 }
 
-// Walk a chunk of nr reads (records in LDS, padded with empty records to 64) with lane = (window
-// g, read slot s): read it*8 + s in iteration it.  NR: the chunk's largest run count (1, 2, 4).
-template <int NR, bool STAGED, bool QUAL, int NC>
+// Walk record of a read (3 x uint4 in LDS, written at chunk load):
+//   [0] = {pos, 4*span, rr0, nb0}  [1] = {rr1, nb1, rr2, nb2}  [2] = {rr3, nb3, 0, 0}
+// M run k: rr = 4*st | 4*en << 16 (empty: st == en), nb = nibble index (staged: relative to the
+// stage) of the base at reference offset 0, i.e. seq_nib + qd.
+__device__ __forceinline__ uint32_t pack_rr(uint32_t st, uint32_t en) { return (st * 4u) | ((en * 4u) << 16); }
+
+// mask of the window nibbles whose reference offsets (from the read start, x4) lie in
+// [lo4, hi4); j4 = 4 * window start
+__device__ __forceinline__ uint32_t range_mask(int lo4, int hi4, int j4) {
+    int kl = lo4 - j4;
+    kl = kl < 0 ? 0 : (kl > 32 ? 32 : kl);
+    int kh = hi4 - j4;
+    kh = kh < kl ? kl : (kh > 32 ? 32 : kh);
+    return lo32_bit(kh) - lo32_bit(kl);
+}
+
+// The 8 event classes (x) one read has in the lane's window [gb, gb + 8): its M runs' bases
+// (one funnel-shifted fetch each) and, GAP, class 1100 on the rest of [0, span).
+template <int NR, bool GAP, bool STAGED, bool QUAL>
+__device__ __forceinline__ uint32_t window_events(const PileArgs& A, const uint4* rec, const uint32_t* words, int r,
+                                                  int gb) {
+    const uint4 a = rec[r * 3];
+    uint4 b = make_uint4(0u, 0u, 0u, 0u);
+    uint2 c = make_uint2(0u, 0u);
+    if (NR > 1) b = rec[r * 3 + 1];
+    if (NR > 3) c = *(const uint2*)&rec[r * 3 + 2];
+    const int j0 = gb - (int)a.x;  // window start relative to the read start
+    const int j4 = j0 * 4;
+    const uint32_t rr[4] = {a.z, b.x, b.z, c.x};
+    const uint32_t nb[4] = {a.w, b.y, b.w, c.y};
+    uint32_t x = 0, mm = 0;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const uint32_t m = range_mask((int)(rr[k] & 0xFFFFu), (int)(rr[k] >> 16), j4);
+        const int64_t n0 = STAGED ? (int64_t)((int)nb[k] + j0) : (int64_t)(int32_t)nb[k] + j0;
+        uint32_t v = fetch8<STAGED>(A, words, n0);
+        if (QUAL && !STAGED) v &= qual_mask_at(A, n0);
+        x |= v & m;
+        if (GAP) mm |= m;
+    }
+    if (GAP) x |= kClsDel & range_mask(0, (int)a.y, j4) & ~mm;
+    return x;
+}
+
+// Walk a chunk of nr reads (records padded with empty ones to 64) with lane = (window g, read
+// slot s): reads it*8 + s and it*8 + 8 + s in step it (two independent LDS chains in flight;
+// rounding the steps up to even only ever touches padding records).  NR: the chunk's largest
+// run count (1, 2, 4).  nr and it4 are wave-uniform.
+template <int NR, bool GAP, bool STAGED, bool QUAL, int NC>
 __device__ __forceinline__ void walk_swar(const PileArgs& A, const uint4* rec, const uint32_t* words, int nr, int gb,
                                           int s8, int64_t rbase, bool edge, uint32_t bmask, Swar& W, int& it4,
                                           uint32_t (&cnt)[6], int64_t& bad) {
-    const int iters = (nr + 7) >> 3;
-    for (int it = 0; it < iters; ++it) {
-        const int r = it * 8 + s8;
-        const uint4 a = rec[r * 2];
-        uint4 b = make_uint4(0u, 0u, 0u, 0u);
-        if (NR > 1) b = rec[r * 2 + 1];
-        const int j0 = gb - (int)a.x;  // window start relative to the read start
-        const int span = (int)(a.z & 0xFFFFu);
-        const int nrun = (int)(a.z >> 16);
-        const uint32_t runs[4] = {a.w, b.x, b.y, b.z};
-        uint32_t x = 0;
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const uint32_t wk = runs[k];
-            const int sk = (int)(wk & 0x1FFFu);
-            const int ek = (k + 1 < NR && k + 1 < nrun) ? (int)(runs[k + 1 < NR ? k + 1 : k] & 0x1FFFu) : span;
-            int kl = sk - j0;
-            kl = kl < 0 ? 0 : (kl > 8 ? 8 : kl);
-            int kh = ek - j0;
-            kh = kh < kl ? kl : (kh > 8 ? 8 : kh);
-            if (NR > 1 && k >= nrun) kh = kl;
-            const uint32_t m = nib_range(kl, kh);
-            const int64_t n0 = (int64_t)a.y + j0 + ((int32_t)wk >> 16);
-            uint32_t v = fetch8<STAGED>(A, words, n0);
-            if (QUAL && !STAGED) v &= qual_mask_at(A, n0);
-            v = (wk & kRunDS) ? kClsDel : v;
-            x |= v & m;
-        }
+    const int iters = (((nr + 7) >> 3) + 1) & ~1;
+    for (int it = 0; it < iters; it += 2) {
+        const int r0 = it * 8 + s8, r1 = r0 + 8;
+        uint32_t x0 = window_events<NR, GAP, STAGED, QUAL>(A, rec, words, r0, gb);
+        uint32_t x1 = window_events<NR, GAP, STAGED, QUAL>(A, rec, words, r1, gb);
         if (edge) {  // events at positions >= L: the reference's out_of_range
-            if ((x & bmask) && rbase + r < bad) bad = rbase + r;
-            x &= ~bmask;
+            if ((x0 & bmask) && rbase + r0 < bad) bad = rbase + r0;
+            if ((x1 & bmask) && rbase + r1 < bad) bad = rbase + r1;
+            x0 &= ~bmask;
+            x1 &= ~bmask;
         }
-        swar_add<NC>(W, x);
-        if (++it4 == 15) {
+        swar_add<NC>(W, x0);
+        swar_add<NC>(W, x1);
+        it4 += 2;
+        if (it4 >= 14) {  // every a4 field <= 14
             swar_fold<NC>(W, cnt, s8);
             it4 = 0;
         }
@@ -436,10 +464,14 @@ __device__ __forceinline__ void walk_swar(const PileArgs& A, const uint4* rec, c
 
 constexpr int kFinBytes = 4 * 6 * kTile * 4;
 
-// dynamic LDS: [rec: nw x 2 KB][stage: nw x kStageRegion][fin: 6 KB][reduction / terms]
+// dynamic LDS: [rec: nw x 3 KB][stage: nw x kStageRegion][fin: 6 KB].  Once a tile's walk is
+// done, a wave's stage region holds its partial counts for the group reduction, and the first
+// wave's region of a group then holds the group's fp64 terms (12 x 64 x 8 B).
+constexpr int kRecBytes = kTile * 3 * 16;
+static_assert(12 * kTile * 8 <= kStageRegion, "terms must fit a stage region");
 __host__ __device__ inline size_t pileup_lds_bytes(int nw, int groups) {
-    const size_t red = (size_t)nw * 6 * kTile * 4, terms = (size_t)groups * 12 * kTile * 8;
-    return (size_t)nw * kTile * 2 * 16 + (size_t)nw * kStageRegion + kFinBytes + (red > terms ? red : terms);
+    (void)groups;
+    return (size_t)nw * (kRecBytes + kStageRegion) + kFinBytes;
 }
 
 template <bool QUAL, int K, bool STATS>
@@ -452,16 +484,22 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     const int g = wave / S, ws = wave - g * S;
     const int groups = nw / S;
     uint4* rec_all = (uint4*)dyn;
-    uint8_t* stage_all = dyn + (size_t)nw * kTile * 2 * 16;
+    uint8_t* stage_all = dyn + (size_t)nw * kRecBytes;
     uint32_t(*fin)[6][kTile] = (uint32_t(*)[6][kTile])(stage_all + (size_t)nw * kStageRegion);
-    uint32_t* red = (uint32_t*)((unsigned char*)fin + kFinBytes);
-    double* terms = (double*)red;
+    // aliases of the stage regions, live only after the walk (see pileup_lds_bytes)
+    auto red_of = [&](int w) { return (uint32_t*)(stage_all + (size_t)w * kStageRegion); };
+    double* terms_g = (double*)(stage_all + (size_t)(g * S) * kStageRegion);
     const int64_t nblk_tiles = (A.n_tiles + groups - 1) / groups;
     const int64_t L = A.L;
     const int s8 = lane & 7;
     const bool qual_vec = ((uintptr_t)A.qual & 15u) == 0;
 
-    for (int64_t bt = blockIdx.x; bt < nblk_tiles; bt += gridDim.x) {
+    // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs; give each XCD a
+    // contiguous run of tiles so neighbouring tiles (which share ~2/3 of their reads) hit the
+    // same L2 instead of fetching the reads' CIGAR / sequence from HBM once per tile
+    const int64_t G = gridDim.x;
+    const int64_t lb = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
+    for (int64_t bt = lb; bt < nblk_tiles; bt += G) {
         const int64_t t = bt * groups + g;
         const int64_t t0 = t * kTile;
         const int64_t P = t0 + lane;
@@ -486,19 +524,20 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
 #pragma unroll
             for (int c = 0; c < 6; ++c) W.a4[c] = 0;
             int it4 = 0;
-            uint4* myrec = rec_all + wave * kTile * 2;
+            uint4* myrec = rec_all + wave * kTile * 3;
             uint8_t* mystage = stage_all + (size_t)wave * kStageRegion + 16;
             for (int64_t base = lo + (int64_t)ws * 64; base < hi; base += (int64_t)S * 64) {
                 const int nr = (int)((hi - base) < 64 ? (hi - base) : 64);
                 // ---- chunk load: per-read fields lane-parallel, CIGAR -> run table (VALU)
                 RunTable T;
                 uint32_t mpos = 0, msn = 0, mcb = 0, mcn = 0;
-                T.nrun = 1;
+                T.nrun = 0;
                 T.complex = false;
+                T.gap = false;
                 T.span = 0;
                 T.qlen = 0;
 #pragma unroll
-                for (int i = 0; i < kMaxRuns; ++i) T.run[i] = 0;
+                for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
                 if (lane < nr) {
                     const int64_t r = base + lane;
                     mpos = (uint32_t)A.pos[r];
@@ -509,13 +548,9 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
 #pragma unroll
                     for (int i = 0; i < kPre; ++i) w[i] = (uint32_t)i < mcn ? A.cigar[mcb + i] : 0u;
                     T = decode_runs(w, mcn);
-                    if (T.nrun == 0) {  // no reference-consuming op: never counts
-                        T.nrun = 1;
-                        T.run[0] = 0;
-                        T.span = 0;
-                    }
                 }
                 const bool cx = __any(T.complex);
+                const bool gap = __any(T.gap);
                 int maxrun = T.nrun;
                 for (int o = 32; o > 0; o >>= 1) {
                     const int v2 = __shfl_xor(maxrun, o);
@@ -566,11 +601,23 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                     }
                 }
                 const uint32_t qbase = staged ? 2u * seg_lo : 0u;
-                myrec[lane * 2] = make_uint4(mpos, msn - qbase, T.span | ((uint32_t)T.nrun << 16), T.run[0]);
-                myrec[lane * 2 + 1] = make_uint4(T.run[1], T.run[2], T.run[3], 0u);
+                if (cx) {  // walk_complex reads {pos, absolute seq_nib}
+                    myrec[lane * 3] = make_uint4(mpos, msn, 0u, 0u);
+                } else {
+                    uint32_t rr[kMaxRuns], nb[kMaxRuns];
+#pragma unroll
+                    for (int k = 0; k < kMaxRuns; ++k) {
+                        rr[k] = pack_rr(T.st[k], T.en[k]);
+                        nb[k] = msn - qbase + (uint32_t)T.qd[k];
+                    }
+                    myrec[lane * 3] = make_uint4(mpos, T.span * 4u, rr[0], nb[0]);
+                    myrec[lane * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
+                    myrec[lane * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
+                }
                 __builtin_amdgcn_wave_barrier();
                 const int64_t rbase = base;
-                if (cx) {
+                if (A.ablate & 4) {
+                } else if (cx) {
                     if (pending + nr >= (1 << kField) - 1) {
                         flush_acc(acc, cnt);
                         pending = 0;
@@ -578,18 +625,24 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                     pending += nr;
                     walk_complex<QUAL>(A, myrec, nr, P, t0, rbase, edge && beyond, mcn, mcb, acc, bad);
                 } else {
-                    const uint32_t* words = staged ? (const uint32_t*)mystage : (const uint32_t*)A.seq;
-#define BC_WALK(NR, ST)                                                                                     \
-    walk_swar<NR, ST, QUAL, K>(A, myrec, words, nr, gb, s8, rbase, edge, bmask, W, it4, cnt, bad)
+                    // separate calls keep the LDS / global address spaces visible to the compiler
+#define BC_WALK(NR, GP, ST)                                                                                 \
+    walk_swar<NR, GP, ST, QUAL, K>(A, myrec, ST ? (const uint32_t*)mystage : (const uint32_t*)A.seq, nr, gb,   \
+                                   s8, rbase, edge, bmask, W, it4, cnt, bad)
+#define BC_WALK_NR(GP, ST)                                                                                  \
+    do {                                                                                                    \
+        if (maxrun <= 1) BC_WALK(1, GP, ST);                                                                \
+        else if (maxrun == 2) BC_WALK(2, GP, ST);                                                           \
+        else BC_WALK(4, GP, ST);                                                                            \
+    } while (0)
                     if (staged) {
-                        if (maxrun == 1) BC_WALK(1, true);
-                        else if (maxrun == 2) BC_WALK(2, true);
-                        else BC_WALK(4, true);
+                        if (gap) BC_WALK_NR(true, true);
+                        else BC_WALK_NR(false, true);
                     } else {
-                        if (maxrun == 1) BC_WALK(1, false);
-                        else if (maxrun == 2) BC_WALK(2, false);
-                        else BC_WALK(4, false);
+                        if (gap) BC_WALK_NR(true, false);
+                        else BC_WALK_NR(false, false);
                     }
+#undef BC_WALK_NR
 #undef BC_WALK
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -607,12 +660,12 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
         // ---- reduce the S waves of the group through LDS
         if (S > 1) {
 #pragma unroll
-            for (int c = 0; c < K; ++c) red[(wave * K + c) * kTile + lane] = cnt[c];
+            for (int c = 0; c < K; ++c) red_of(wave)[c * kTile + lane] = cnt[c];
             __syncthreads();
             if (ws == 0)
                 for (int w2 = wave + 1; w2 < wave + S; ++w2) {
 #pragma unroll
-                    for (int c = 0; c < K; ++c) cnt[c] += red[(w2 * K + c) * kTile + lane];
+                    for (int c = 0; c < K; ++c) cnt[c] += red_of(w2)[c * kTile + lane];
                 }
         }
         const bool own = t < A.n_tiles && t0 < L && !(A.ablate & 16);  // tile holds real positions
@@ -633,7 +686,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
         }
         __syncthreads();
         // ---- fused kernel 2: per-lane fp64 terms, then ordered sums per position
-        if (own) tile_terms<K>(A, &fin[g][0][0], terms + g * 2 * K * kTile, t0, ws * 64 + lane, S * 64);
+        if (own) tile_terms<K>(A, &fin[g][0][0], terms_g, t0, ws * 64 + lane, S * 64);
         __syncthreads();
         if (own && ws == 0 && P < L) {
             int64_t cov = 0;
@@ -649,13 +702,13 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                 double s = 0.0;
 #pragma unroll
                 for (int j = 0; j < K; ++j)
-                    if (cnt[j] != 0) s = s + terms[(g * 2 * K + j) * kTile + lane];
+                    if (cnt[j] != 0) s = s + terms_g[j * kTile + lane];
                 h = A.nf * s;
                 if (cov - (int64_t)mx != 0) {
                     double s2 = 0.0;
 #pragma unroll
                     for (int j = 0; j < K; ++j) {
-                        const double tj = terms[(g * 2 * K + K + j) * kTile + lane];
+                        const double tj = terms_g[(K + j) * kTile + lane];
                         if (tj != 0.0) s2 = s2 + tj;
                     }
                     h2 = A.nf2 * s2;
@@ -718,6 +771,7 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
     int64_t blocks = (A.n_tiles + groups - 1) / groups;
     const int64_t cap = 256 * 64;
     if (blocks > cap) blocks = cap;
+    blocks = (blocks + 7) / 8 * 8;  // a multiple of the XCD count (see the kernel's tile mapping)
     const dim3 grid((unsigned)blocks), block(64 * nw);
     const size_t lds = pileup_lds_bytes(nw, groups);
     // > 64 KiB of dynamic LDS must be allowed per kernel (160 KiB per CU on gfx950)

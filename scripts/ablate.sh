@@ -1,8 +1,8 @@
 #!/bin/bash
+# Kernel-time ablations (BC_ABLATE bits, diagnostic only): ABL="0 4 32" CFGS="c2 c3" bash scripts/ablate.sh
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
-for S in 1 8; do for AB in 0 3 11 27 24 4 28; do
-  echo "c2 S=$S ablate=$AB $(BC_TILE_WAVES=$S BC_ABLATE=$AB timeout -k 10 300 python bench.py --config c2 --no-cpu-baseline --steps 100 --warmup 3 | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["pileup_kernel_us"],1), round(d["ms_per_step"]*1e3,1))')" || exit 1
+for c in ${CFGS:-c2 c3}; do for a in ${ABL:-0 4 32 1}; do
+  BC_ABLATE=$a timeout -k 10 300 python bench.py --config $c --no-cpu-baseline --steps 50 --warmup 5 ${BENCH_ARGS} > gpurun_out/abl_${c}_$a.log 2>&1
+  rc=$?; case $rc in 124|134|137|139) echo "FATAL $rc"; exit $rc;; esac
+  python3 -c "import json,sys; l=[x for x in open('gpurun_out/abl_${c}_$a.log') if x.startswith('{')]; d=json.loads(l[-1]) if l else {}; print('$c ablate $a', round(d.get('pileup_kernel_us',-1),2), 'parity', d.get('parity_vs_oracle'))"
 done; done
-cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-BC_TILE_WAVES=8 BC_ABLATE=27 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof27 -o run -- python bench.py --no-cpu-baseline --steps 100 --warmup 3 > /dev/null 2>&1
-cat gpurun_out/prof27/run_kernel_stats.csv | cut -c1-160

@@ -113,7 +113,7 @@ struct RunTable {
     bool complex;
 };
 
-__device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn) {
+__device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn, int cmax) {
     RunTable T;
 #pragma unroll
     for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
@@ -124,6 +124,7 @@ __device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint3
     int last_qd = 0;
 #pragma unroll
     for (int k = 0; k < kPre; ++k) {
+        if (k >= cmax) break;  // wave-uniform: no lane has more ops
         if ((uint32_t)k < cn) {
             const uint32_t op = w[k] & 15u, len = w[k] >> 4;
             if (mlike(op) && len) {
@@ -156,6 +157,19 @@ __device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint3
     T.span = rc;
     T.qlen = qc;
     return T;
+}
+
+// Wave-wide max / min (result in every lane's SGPR): DPP row prefix, row broadcasts, readlane.
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
+    auto op = [](uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // First indices with pos >= v_lo (lanes 0-31) and pos >= v_hi (lanes 32-63), searched together:
@@ -544,19 +558,21 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                     mcb = A.cig_beg[r];
                     mcn = A.cig_n[r];
                     msn = A.seq_nib[r];
+                }
+                // ops to decode: the wave's largest CIGAR (more than kPre -> complex anyway)
+                const int cmax = (int)wave_reduce<true>(mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre);
+                if (lane < nr) {
                     uint32_t w[kPre];
 #pragma unroll
-                    for (int i = 0; i < kPre; ++i) w[i] = (uint32_t)i < mcn ? A.cigar[mcb + i] : 0u;
-                    T = decode_runs(w, mcn);
+                    for (int i = 0; i < kPre; ++i) {
+                        w[i] = 0u;
+                        if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
+                    }
+                    T = decode_runs(w, mcn, cmax);
                 }
                 const bool cx = __any(T.complex);
                 const bool gap = __any(T.gap);
-                int maxrun = T.nrun;
-                for (int o = 32; o > 0; o >>= 1) {
-                    const int v2 = __shfl_xor(maxrun, o);
-                    maxrun = v2 > maxrun ? v2 : maxrun;
-                }
-                maxrun = __builtin_amdgcn_readfirstlane(maxrun);
+                const int maxrun = (int)wave_reduce<true>((uint32_t)T.nrun);
                 // ---- stage the chunk's sequence (BC_SEQ_EVENT words) into LDS; with a quality
                 // threshold, bases below it are cleared here (count.cpp:56)
                 uint32_t blo = 0xFFFFFFFFu, bhi = 0;
@@ -564,13 +580,8 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                     blo = msn >> 1;
                     bhi = (msn + T.qlen + 1) >> 1;
                 }
-                for (int o = 32; o > 0; o >>= 1) {
-                    const uint32_t l2 = __shfl_xor(blo, o), h2 = __shfl_xor(bhi, o);
-                    blo = l2 < blo ? l2 : blo;
-                    bhi = h2 > bhi ? h2 : bhi;
-                }
-                uint32_t seg_lo = __builtin_amdgcn_readfirstlane(blo);
-                const uint32_t seg_hi = __builtin_amdgcn_readfirstlane(bhi);
+                uint32_t seg_lo = wave_reduce<false>(blo);
+                const uint32_t seg_hi = wave_reduce<true>(bhi);
                 seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
                 const bool staged = !cx && seg_hi - seg_lo <= (uint32_t)kStage && !(A.ablate & 32);
                 if (staged) {

@@ -1,8 +1,8 @@
 #!/bin/bash
+# Waves-per-tile sweep (BC_TILE_WAVES): CFGS="c2 c3" SS="2 4 8" bash scripts/sweep_s.sh
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -k "fused or kernel1 or full_size or smoke" > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log
-case $rc in 124|134|137|139) exit $rc;; esac
-for C in c2 c3; do for S in 4 8; do for AB in 0 3; do
-  st=100; [ $C = c3 ] && st=20
-  echo "$C S=$S ab=$AB $(BC_ABLATE=$AB BC_TILE_WAVES=$S timeout -k 10 300 python bench.py --config $C --no-cpu-baseline --steps $st --warmup 3 | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["pileup_kernel_us"],1), round(d["ms_per_step"]*1e3,1), d["parity_vs_oracle"])')" || exit 1
-done; done; done
+for C in ${CFGS:-c2 c3}; do for S in ${SS:-2 4 8}; do
+  BC_TILE_WAVES=$S timeout -k 10 300 python bench.py --config $C --no-cpu-baseline --steps 50 --warmup 5 > gpurun_out/sw_${C}_$S.log 2>&1
+  rc=$?; case $rc in 124|134|137|139) echo "FATAL $rc"; exit $rc;; esac
+  python3 -c "import json; l=[x for x in open('gpurun_out/sw_${C}_$S.log') if x.startswith('{')]; d=json.loads(l[-1]) if l else {}; print('$C S=$S', round(d.get('pileup_kernel_us',-1),2), 'parity', d.get('parity_vs_oracle'))"
+done; done

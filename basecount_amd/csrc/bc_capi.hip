@@ -205,6 +205,8 @@ int bc_ctx_destroy(bc_ctx* c) {
             (void)hipEventDestroy(pr.first);
             (void)hipEventDestroy(pr.second);
         }
+    for (auto& e : c->mark)
+        if (e) (void)hipEventDestroy(e);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return BC_OK;
@@ -423,6 +425,24 @@ int bc_timing_report(bc_ctx* c, int64_t* launches, double* mean_us) {
         mean_us[id] = c->ev[id].empty() ? 0.0 : tot * 1e3 / (double)c->ev[id].size();
         c->ev[id].clear();
     }
+    return BC_OK;
+}
+
+int bc_event_record(bc_ctx* c, int slot) {
+    if (!c || slot < 0 || slot >= BC_EVENT_SLOTS) return fail(BC_E_ARG, "bad context or event slot");
+    DeviceGuard g(c->device);
+    if (!c->mark[slot]) HIP_TRY(hipEventCreate(&c->mark[slot]));
+    HIP_TRY(hipEventRecord(c->mark[slot], c->stream));
+    return BC_OK;
+}
+
+int bc_event_elapsed_ms(bc_ctx* c, int s0, int s1, float* ms) {
+    if (!c || !ms || s0 < 0 || s1 < 0 || s0 >= BC_EVENT_SLOTS || s1 >= BC_EVENT_SLOTS)
+        return fail(BC_E_ARG, "bad context, slot or output");
+    if (!c->mark[s0] || !c->mark[s1]) return fail(BC_E_ARG, "event slot never recorded");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipEventSynchronize(c->mark[s1]));
+    HIP_TRY(hipEventElapsedTime(ms, c->mark[s0], c->mark[s1]));
     return BC_OK;
 }
 

@@ -19,6 +19,7 @@ struct bc_ctx {
     unsigned long long* h_err = nullptr;  // pinned mirror
     bool timing = false;                  // bc_timing_enable: hipEvents around every launch
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[BC_KERNEL_IDS];
+    hipEvent_t mark[BC_EVENT_SLOTS] = {};   // bc_event_record slots (created on first use)
 };
 
 struct bc_graph {

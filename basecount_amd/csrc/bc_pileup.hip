@@ -24,26 +24,14 @@
 namespace bc {
 namespace {
 
+constexpr int kStage = 6144;     // LDS bytes per wave for a chunk's sequence (64 reads x <= 190 bp)
+#include "bc_walk.h"
+
 constexpr int kTile = 64;
-// BC_SEQ_EVENT class -> count column (A0 C1 G2 T3 N5); 6 = not counted (junk field).
-// The classes are count.cpp:58-65's letters through pysam's "=ACMGRSVTWYHKDBN" decode.
-constexpr unsigned long long kNibCol6 = 0x6666666366625106ull;
-constexpr uint32_t kM1 = 0x11111111u;   // bit 0 of every nibble
-constexpr uint32_t kClsDel = 0xCCCCCCCCu;  // class 1100 (deletion / ref-skip) in every nibble
 constexpr int kField = 10;  // packed counter: six 10-bit fields + junk at bit 60; flush < 1024
 constexpr int kJunk = 60;
 constexpr int kBatch = 8;   // reads whose sequence loads are in flight together
-constexpr int kPre = 8;     // CIGAR words decoded per read at chunk load (more -> complex path)
-constexpr int kStage = 6144;     // LDS bytes per wave for a chunk's sequence (64 reads x <= 190 bp)
 constexpr int kStageRegion = kStage + 32;  // + one 16-byte pad before and after
-constexpr uint32_t kNone = 0xFFFFFFFFu;  // packed event: none
-constexpr uint32_t kDel = 0x80000000u;   // packed event: deletion / ref-skip
-
-__device__ __forceinline__ unsigned nib_col6(unsigned nib) { return (unsigned)(kNibCol6 >> (nib * 4)) & 0xFu; }
-__device__ __forceinline__ bool mlike(uint32_t op) { return op == 0 || op == 7 || op == 8; }
-__device__ __forceinline__ bool dlike(uint32_t op) { return op == 2 || op == 3; }
-__device__ __forceinline__ bool qcons(uint32_t op) { return op == 0 || op == 1 || op == 7 || op == 8; }
-__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
 struct PileArgs {
     const int32_t* pos;
@@ -94,82 +82,6 @@ __device__ __forceinline__ uint32_t resolve_slow(int j, int jlo, uint32_t cn, ui
         if (qcons(op)) qc += len;
     }
     return e;
-}
-
-// Run table of a read: its aligned (M/=/X) bases as at most 4 runs [st, en) of reference
-// offsets from the read start, each with a query delta qd (query offset = reference offset +
-// qd; consecutive M/=/X ops with the same delta merge, so the M/=/X distinction and S/H/P
-// between them vanish).  Every other reference offset in [0, span) is a deletion / ref-skip.
-// count.cpp:40-96 semantics: M/=/X consume both, I the query only, D/N the reference only.
-constexpr int kMaxRuns = 4;
-
-struct RunTable {
-    uint32_t st[kMaxRuns], en[kMaxRuns];
-    int32_t qd[kMaxRuns];
-    uint32_t span;
-    uint32_t qlen;  // query bases consumed (M/=/X/I) by the decoded ops
-    int nrun;
-    bool gap;       // some reference offset in [0, span) is a deletion / ref-skip
-    bool complex;
-};
-
-__device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn, int cmax) {
-    RunTable T;
-#pragma unroll
-    for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
-    T.nrun = 0;
-    T.gap = false;
-    T.complex = cn > (uint32_t)kPre;
-    uint32_t rc = 0, qc = 0, last_en = 0xFFFFFFFFu;
-    int last_qd = 0;
-#pragma unroll
-    for (int k = 0; k < kPre; ++k) {
-        if (k >= cmax) break;  // wave-uniform: no lane has more ops
-        if ((uint32_t)k < cn) {
-            const uint32_t op = w[k] & 15u, len = w[k] >> 4;
-            if (mlike(op) && len) {
-                const int qd = (int)qc - (int)rc;
-                if (qd < -32768 || qd > 32767) T.complex = true;
-                if (last_en == rc && last_qd == qd) {  // extends the previous run
-#pragma unroll
-                    for (int i = 0; i < kMaxRuns; ++i)
-                        if (T.nrun - 1 == i) T.en[i] = rc + len;
-                } else {
-                    if (T.nrun >= kMaxRuns) T.complex = true;
-#pragma unroll
-                    for (int i = 0; i < kMaxRuns; ++i)
-                        if (T.nrun == i) T.st[i] = rc, T.en[i] = rc + len, T.qd[i] = qd;
-                    ++T.nrun;
-                }
-                rc += len;
-                qc += len;
-                last_en = rc;
-                last_qd = qd;
-            } else if (dlike(op) && len) {
-                T.gap = true;
-                rc += len;
-            } else if (op == 1) {
-                qc += len;
-            }
-        }
-    }
-    if (rc >= 0x1FFFu) T.complex = true;
-    T.span = rc;
-    T.qlen = qc;
-    return T;
-}
-
-// Wave-wide max / min (result in every lane's SGPR): DPP row prefix, row broadcasts, readlane.
-template <bool MAX>
-__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
-    auto op = [](uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // First indices with pos >= v_lo (lanes 0-31) and pos >= v_hi (lanes 32-63), searched together:
@@ -316,137 +228,6 @@ __device__ __forceinline__ void walk_complex(const PileArgs& A, const uint4* rec
     }
 }
 
-// ---- SWAR counters of a lane's 8-position window ------------------------------------------
-// a4[c]: nibble k = count of column c at window position k; at most 15 reads are added before
-// the wave folds them into cnt[] (a sum over the 8 read slots is then <= 120: fits a byte).
-struct Swar {
-    uint32_t a4[6];
-};
-
-__device__ __forceinline__ uint32_t lo32_bit(int sh) { return (uint32_t)(1ull << sh); }  // sh in [0, 32]
-// nibbles [kl, kh) of a window word, 0 <= kl <= kh <= 8
-__device__ __forceinline__ uint32_t nib_range(int kl, int kh) { return lo32_bit(4 * kh) - lo32_bit(4 * kl); }
-
-template <int NC>
-__device__ __forceinline__ void swar_add(Swar& W, uint32_t x) {
-    const uint32_t x1 = x >> 1, x2 = x >> 2, x3 = x >> 3;
-    W.a4[0] += x & ~x1 & kM1;   // A  0001
-    W.a4[1] += x1 & ~x & kM1;   // C  0010
-    W.a4[2] += x2 & ~x3 & kM1;  // G  0100
-    W.a4[3] += x3 & ~x2 & kM1;  // T  1000
-    W.a4[4] += x2 & x3 & kM1;   // DS 1100
-    if (NC == 6) W.a4[5] += x & x1 & kM1;  // N 0011
-}
-
-// sum over the 8 read slots (lanes 8g .. 8g+7): quad xor 1, quad xor 2, half-row mirror
-__device__ __forceinline__ uint32_t sum8(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
-    return v;
-}
-
-// Fold the window counters into cnt[] of this lane's own position (8g + s == lane).  Must be
-// called by the whole wave.  Byte b of the even / odd half holds window position 2b / 2b + 1.
-template <int NC>
-__device__ __forceinline__ void swar_fold(Swar& W, uint32_t (&cnt)[6], int s8) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const uint32_t b0 = sum8(W.a4[c] & 0x0F0F0F0Fu), b1 = sum8((W.a4[c] >> 4) & 0x0F0F0F0Fu);
-        cnt[c] += (((s8 & 1) ? b1 : b0) >> (8 * (s8 >> 1))) & 0xFFu;
-        W.a4[c] = 0;
-    }
-}
-
-// SWAR mask of 8 bases that pass the quality test, from their 8 quality bytes (q0: bases 0-3).
-__device__ __forceinline__ uint32_t ge_bytes(uint32_t q, uint32_t m) {  // per byte q >= m, m in [1, 255]
-    const uint32_t H = 0x80808080u;
-    const uint32_t t = (q | H) - (m & 0x7Fu) * 0x01010101u;  // high bit: low7(q) >= low7(m)
-    return (m & 0x80u) ? (q & t & H) : ((q | t) & H);
-}
-__device__ __forceinline__ uint32_t qual_nibmask(uint32_t q0, uint32_t q1, uint32_t m) {
-    if (m > 255u) return 0u;
-    uint32_t b0 = (ge_bytes(q0, m) >> 7) * 15u, b1 = (ge_bytes(q1, m) >> 7) * 15u;
-    b0 |= b0 >> 4;
-    b1 |= b1 >> 4;
-    return __builtin_amdgcn_perm(b1, b0, 0x06040200u);
-}
-
-// The 8 event classes at nibble indices n0 .. n0+7 of the sequence (unstaged: global memory).
-template <bool STAGED>
-__device__ __forceinline__ uint32_t fetch8(const PileArgs& A, const uint32_t* words, int64_t n0) {
-    if (STAGED) {
-        // staged words have one readable pad word before and after; windows that matter have
-        // n0 >= -7, anything else is masked off after the fetch
-        const int n = (int)n0;
-        int w0 = n >> 3;
-        w0 = w0 < -1 ? -1 : (w0 > kStage / 4 ? kStage / 4 : w0);
-        return __builtin_amdgcn_alignbit(words[w0 + 1], words[w0], (uint32_t)n << 2);
-    }
-    const int64_t w0 = n0 >> 3, nw = A.seq_words;
-    const int64_t i0 = w0 < 0 ? 0 : (w0 >= nw ? nw - 1 : w0);
-    const int64_t i1 = w0 + 1 < 0 ? 0 : (w0 + 1 >= nw ? nw - 1 : w0 + 1);
-    const uint32_t lo = (w0 >= 0 && w0 < nw) ? words[i0] : 0u;
-    const uint32_t hi = (w0 + 1 >= 0 && w0 + 1 < nw) ? words[i1] : 0u;
-    uint32_t v = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(n0 & 7) * 4u);
-    return v;
-}
-
-// quality mask of bases n0 .. n0+7 (unstaged chunks only; staged ones are masked at staging)
-__device__ __forceinline__ uint32_t qual_mask_at(const PileArgs& A, int64_t n0) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int64_t i = n0 + k;
-        if (i >= 0 && i < A.qual_bytes && (uint32_t)A.qual[i] >= A.mbq) m |= 0xFu << (4 * k);
-    }
-    return m;
-}
-
-// Walk record of a read (3 x uint4 in LDS, written at chunk load):
-//   [0] = {pos, 4*span, rr0, nb0}  [1] = {rr1, nb1, rr2, nb2}  [2] = {rr3, nb3, 0, 0}
-// M run k: rr = 4*st | 4*en << 16 (empty: st == en), nb = nibble index (staged: relative to the
-// stage) of the base at reference offset 0, i.e. seq_nib + qd.
-__device__ __forceinline__ uint32_t pack_rr(uint32_t st, uint32_t en) { return (st * 4u) | ((en * 4u) << 16); }
-
-// mask of the window nibbles whose reference offsets (from the read start, x4) lie in
-// [lo4, hi4); j4 = 4 * window start
-__device__ __forceinline__ uint32_t range_mask(int lo4, int hi4, int j4) {
-    int kl = lo4 - j4;
-    kl = kl < 0 ? 0 : (kl > 32 ? 32 : kl);
-    int kh = hi4 - j4;
-    kh = kh < kl ? kl : (kh > 32 ? 32 : kh);
-    return lo32_bit(kh) - lo32_bit(kl);
-}
-
-// The 8 event classes (x) one read has in the lane's window [gb, gb + 8): its M runs' bases
-// (one funnel-shifted fetch each) and, GAP, class 1100 on the rest of [0, span).
-template <int NR, bool GAP, bool STAGED, bool QUAL>
-__device__ __forceinline__ uint32_t window_events(const PileArgs& A, const uint4* rec, const uint32_t* words, int r,
-                                                  int gb) {
-    const uint4 a = rec[r * 3];
-    uint4 b = make_uint4(0u, 0u, 0u, 0u);
-    uint2 c = make_uint2(0u, 0u);
-    if (NR > 1) b = rec[r * 3 + 1];
-    if (NR > 3) c = *(const uint2*)&rec[r * 3 + 2];
-    const int j0 = gb - (int)a.x;  // window start relative to the read start
-    const int j4 = j0 * 4;
-    const uint32_t rr[4] = {a.z, b.x, b.z, c.x};
-    const uint32_t nb[4] = {a.w, b.y, b.w, c.y};
-    uint32_t x = 0, mm = 0;
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-        const uint32_t m = range_mask((int)(rr[k] & 0xFFFFu), (int)(rr[k] >> 16), j4);
-        const int64_t n0 = STAGED ? (int64_t)((int)nb[k] + j0) : (int64_t)(int32_t)nb[k] + j0;
-        uint32_t v = fetch8<STAGED>(A, words, n0);
-        if (QUAL && !STAGED) v &= qual_mask_at(A, n0);
-        x |= v & m;
-        if (GAP) mm |= m;
-    }
-    if (GAP) x |= kClsDel & range_mask(0, (int)a.y, j4) & ~mm;
-    return x;
-}
-
 // Walk a chunk of nr reads (records padded with empty ones to 64) with lane = (window g, read
 // slot s): reads it*8 + s and it*8 + 8 + s in step it (two independent LDS chains in flight;
 // rounding the steps up to even only ever touches padding records).  NR: the chunk's largest
@@ -455,11 +236,12 @@ template <int NR, bool GAP, bool STAGED, bool QUAL, int NC>
 __device__ __forceinline__ void walk_swar(const PileArgs& A, const uint4* rec, const uint32_t* words, int nr, int gb,
                                           int s8, int64_t rbase, bool edge, uint32_t bmask, Swar& W, int& it4,
                                           uint32_t (&cnt)[6], int64_t& bad) {
+    const SeqSrc src{words, STAGED ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
     const int iters = (((nr + 7) >> 3) + 1) & ~1;
     for (int it = 0; it < iters; it += 2) {
         const int r0 = it * 8 + s8, r1 = r0 + 8;
-        uint32_t x0 = window_events<NR, GAP, STAGED, QUAL>(A, rec, words, r0, gb);
-        uint32_t x1 = window_events<NR, GAP, STAGED, QUAL>(A, rec, words, r1, gb);
+        uint32_t x0 = window_events<NR, GAP, STAGED, QUAL>(src, rec, r0, gb);
+        uint32_t x1 = window_events<NR, GAP, STAGED, QUAL>(src, rec, r1, gb);
         if (edge) {  // events at positions >= L: the reference's out_of_range
             if ((x0 & bmask) && rbase + r0 < bad) bad = rbase + r0;
             if ((x1 & bmask) && rbase + r1 < bad) bad = rbase + r1;
@@ -491,6 +273,7 @@ __host__ __device__ inline size_t pileup_lds_bytes(int nw, int groups) {
 template <bool QUAL, int K, bool STATS>
 __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    if (A.ablate & 64) return;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nw = blockDim.x >> 6;

@@ -86,6 +86,8 @@ def lib() -> C.CDLL:
         "bc_graph_destroy": ([vp], C.c_int),
         "bc_timing_enable": ([vp, C.c_int], C.c_int),
         "bc_timing_report": ([vp, vp, vp], C.c_int),
+        "bc_event_record": ([vp, C.c_int], C.c_int),
+        "bc_event_elapsed_ms": ([vp, C.c_int, C.c_int, C.POINTER(C.c_float)], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -256,6 +258,15 @@ class Context:
         """BAM-packed sequence -> BC_SEQ_EVENT (d_event may alias d_bam; it needs
         seq_event_bytes(seq_bytes) bytes)."""
         check(lib().bc_seq_to_event(self.h, d_bam, int(seq_bytes), d_event))
+
+    def event_record(self, slot: int) -> None:
+        """Record hipEvent `slot` on the context's stream (region timing)."""
+        check(lib().bc_event_record(self.h, int(slot)))
+
+    def event_elapsed_ms(self, slot0: int, slot1: int) -> float:
+        ms = C.c_float(0.0)
+        check(lib().bc_event_elapsed_ms(self.h, int(slot0), int(slot1), C.byref(ms)))
+        return float(ms.value)
 
     def range_error(self) -> int:
         v = C.c_int64(-1)

@@ -163,6 +163,13 @@ int bc_graph_destroy(bc_graph* g);
 int bc_timing_enable(bc_ctx* ctx, int on);
 int bc_timing_report(bc_ctx* ctx, int64_t* launches /* [BC_KERNEL_IDS] */, double* mean_us /* [..] */);
 
+/* Region timing: bc_event_record(ctx, slot) records hipEvent `slot` (0 .. BC_EVENT_SLOTS-1) on the
+ * context's stream; bc_event_elapsed_ms synchronises on the later one and returns the time
+ * between two recorded slots.  Measures a whole sequence of launches (e.g. K steps) on-device. */
+#define BC_EVENT_SLOTS 4
+int bc_event_record(bc_ctx* ctx, int slot);
+int bc_event_elapsed_ms(bc_ctx* ctx, int slot0, int slot1, float* ms);
+
 /* Blocking: returns the smallest read index that produced an out-of-range counted event since
  * the last call (or -1) and clears the record.                                                 */
 int bc_range_error(bc_ctx* ctx, int64_t* first_bad_read);

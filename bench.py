@@ -32,15 +32,16 @@ WORKLOADS = {
 }
 
 
-def kernel1_bytes(b: dict, L: int, ncols: int, mbq: int, l_seq: np.ndarray) -> int:
-    """Algorithmic HBM bytes of one kernel-1 launch: per read 16 B of
+def pileup_bytes(b: dict, L: int, k: int, mbq: int, l_seq: np.ndarray, with_pc: bool = True) -> int:
+    """Algorithmic HBM bytes of one fused k_pileup launch (roofline): per read 16 B of
     read index (pos, cig_beg, cig_n, seq_nib) + 4 B per CIGAR word + ceil(l_seq/2) B of packed
-    SEQ (+ l_seq B of QUAL when mbq > 0), plus the 4*ncols*L histogram written once."""
+    SEQ (+ l_seq B of QUAL when mbq > 0); per position the outputs written once: k int32 counts,
+    int32 coverage, k f64 percentages (when requested), f64 entropy and secondary entropy."""
     n = int(b["pos"].size)
     per_read = 16 * n + 4 * int(b["cig_n"].sum()) + int(((l_seq + 1) // 2).sum())
     if mbq > 0:
         per_read += int(l_seq.sum())
-    return per_read + 4 * ncols * L
+    return per_read + L * (4 * k + 4 + (8 * k if with_pc else 0) + 16)
 
 
 def cpu_baseline(rs, b, L: int, budget_s: float = 10.0) -> dict:
@@ -193,14 +194,14 @@ def main():
     events = synth.ref_events(rs)
     ms = elapsed / args.steps * 1e3
     positions = world * L * args.steps
-    kbytes = kernel1_bytes(b, L, ncols, args.mbq, rs.l_seq)
+    kbytes = pileup_bytes(b, L, k, args.mbq, rs.l_seq)
     achieved = kbytes / k1 / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "kernel1_pmc.json")
     if os.path.exists(pmc):
         with open(pmc) as fh:
-            pm = json.load(fh)
-        if pm.get("config") == args.config and pm.get("mbq", 0) == args.mbq:
+            pm = json.load(fh).get(args.config, {})
+        if pm and pm.get("mbq", 0) == args.mbq:
             traffic = pm.get("hbm_bytes_per_launch")
 
     if rank == 0:

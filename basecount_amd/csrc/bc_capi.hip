@@ -332,7 +332,13 @@ int bc_count(bc_ctx* c, const bc_reads* r, int64_t ref_len, uint32_t mbq, int nc
     if (!d_hist && ref_len > 0) return fail(BC_E_ARG, "d_hist is NULL");
     if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
     DeviceGuard g(c->device);
-    if (r->sorted && r->max_span <= bc::kTileMaxSpan && r->seq_layout == BC_SEQ_EVENT && !((uintptr_t)r->seq & 15u)) {
+    const bool event = r->seq_layout == BC_SEQ_EVENT && !((uintptr_t)r->seq & 15u);
+    if (r->sorted && event && bc::use_rc(*r, ref_len)) {
+        Timed tm(c, BC_K_RC);
+        HIP_TRY(bc::launch_rc(c->stream, *r, ref_len, mbq, ncols, d_hist, c->d_err));
+        return BC_OK;
+    }
+    if (r->sorted && r->max_span <= bc::kTileMaxSpan && event) {
         // sorted batch: the tiled kernel in accumulate mode (plain read-add-write per owned tile)
         Timed tm(c, BC_K_PILEUP);
         HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, ref_len, r->max_end, mbq, ncols, false, true, 0.0, 0.0,
@@ -360,6 +366,17 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
         return fail(BC_E_ARG, "bc_pileup needs a 16-byte aligned sequence buffer");
     if (L > 0 && (!d_counts || !d_cov || !d_ent || !d_sec)) return fail(BC_E_ARG, "NULL output");
     DeviceGuard g(c->device);
+    if (bc::use_rc(*r, L)) {
+        // deep batch: counts by the read-chunked kernel (atomics into zeroed counts), then kernel 2
+        if (L > 0) HIP_TRY(hipMemsetAsync(d_counts, 0, (size_t)k * (size_t)L * 4, c->stream));
+        {
+            Timed tm(c, BC_K_RC);
+            HIP_TRY(bc::launch_rc(c->stream, *r, L, mbq, k, d_counts, c->d_err));
+        }
+        Timed tm(c, BC_K_STATS);
+        HIP_TRY(bc::launch_stats(c->stream, d_counts, L, k, nf, nf2, d_cov, d_pc, d_ent, d_sec));
+        return BC_OK;
+    }
     Timed tm(c, BC_K_PILEUP);
     HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, d_counts, d_cov,
                                     d_pc, d_ent, d_sec, c->d_err));

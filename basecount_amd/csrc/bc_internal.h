@@ -48,6 +48,12 @@ hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, do
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
                                double* pc, double* ent, double* sec, unsigned long long* d_err);
+hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, int ncols, int32_t* counts,
+                     unsigned long long* d_err);
+// bc_pileup / bc_count choose the read-chunked k_rc over the tiled k_pileup when a tile would
+// walk at least this many reads (deep batches; BC_PILEUP_PATH=tile|rc overrides)
+constexpr double kRcMinReadsPerTile = 2048.0;
+bool use_rc(const bc_reads& r, int64_t L);
 constexpr int kTileMaxSpan = 4096;  // beyond this span the tiled kernel's look-back gets too long
 size_t summary_work_bytes(int64_t L);
 hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,

@@ -1,0 +1,410 @@
+// bc_rc.hip — read-chunked kernel 1 for deep, coordinate-sorted batches (count.cpp:22-97).
+//
+// The position-tiled k_pileup decodes and stages every read once per 64-position tile it
+// overlaps (~(span + 63) / 64 times: 3.3x for 150 bp reads).  At high depth that repeated setup
+// and its HBM traffic dominate.  Here a 256-thread block takes 256 CONSECUTIVE reads of the
+// sorted batch (a chunk), so each read is loaded, CIGAR-decoded and staged exactly once:
+//
+//   1. thread i: read c0 + i -> run table (bc_walk.h) -> 48 B record in LDS; the chunk's packed
+//      sequence (BC_SEQ_EVENT, bases below min_base_quality cleared) is staged into LDS;
+//   2. the chunk covers reference positions [P0, P1); they are cut into 8-position windows and
+//      the (window, 64-read slice) work items are split contiguously over the 4 waves, so a wave
+//      changes window only a few times per chunk (its counter folds stay wave-uniform);
+//   3. lane = read of the slice: the window's 8 event classes are one funnel shift per run, the
+//      six columns are SWAR nibble counters; a fold sums the 8 lanes of a group with DPP and adds
+//      the totals into an LDS histogram of the chunk's positions (16-bit column pairs);
+//   4. the LDS histogram is flushed into the int32 counts with coalesced global atomics (a
+//      position receives one add per chunk overlapping it).
+//
+// Reads with more than 8 CIGAR ops / 4 runs / huge spans are walked separately with global
+// atomics.  Counted events at positions >= L are the reference's std::out_of_range
+// (count.cpp:60-65,85): the first offending read index is kept (atomicMin), nothing is counted
+// there.  Kernel 2 (k_stats) runs afterwards on the counts.
+#include <cstring>
+
+#include "bc_internal.h"
+
+namespace bc {
+namespace {
+
+constexpr int kRcThreads = 256;
+constexpr int kRcReads = 256;   // reads per chunk (one per thread at setup)
+constexpr int kStage = 19968;   // staged sequence bytes per chunk (256 reads x 150 bp fit)
+#include "bc_walk.h"
+
+constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
+constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
+constexpr int kRcWaves = kRcThreads / 64;
+
+struct RcArgs {
+    const int32_t* pos;
+    const uint32_t* cig_beg;
+    const uint32_t* cig_n;
+    const uint32_t* seq_nib;
+    const uint32_t* cigar;
+    const uint8_t* seq;
+    const uint8_t* qual;
+    int64_t n;
+    int64_t L;
+    uint32_t mbq;
+    int64_t seq_words;
+    int64_t qual_bytes;
+    int64_t n_chunks;
+    int32_t* counts;  // [ncols][L], accumulated into
+    unsigned long long* err;
+};
+
+// Block-wide reduction of 8 values (max or min per slot): wave reduce, then LDS across waves.
+// Must be called by the whole block.
+template <int NV>
+__device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const uint32_t r = is_max[k] ? wave_reduce<true>(v[k]) : wave_reduce<false>(v[k]);
+        if (lane == 0) red[wave][k] = r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        uint32_t r = red[0][k];
+        for (int w = 1; w < kRcWaves; ++w) {
+            const uint32_t o = red[w][k];
+            r = is_max[k] ? (o > r ? o : r) : (o < r ? o : r);
+        }
+        v[k] = r;
+    }
+}
+
+// Fold a wave's window counters into the LDS histogram: 8-slot sums per lane group (DPP), then
+// each lane adds its own window position (s = lane & 7) for every column.
+template <int NC>
+__device__ __forceinline__ void rc_fold(Swar& W, uint32_t (*hist)[kRcWinPos], int g, int s8) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t b0 = sum8(W.a4[c] & 0x0F0F0F0Fu), b1 = sum8((W.a4[c] >> 4) & 0x0F0F0F0Fu);
+        const uint32_t v = (((s8 & 1) ? b1 : b0) >> (8 * (s8 >> 1))) & 0xFFu;
+        if (v) atomicAdd(&hist[c >> 1][8 * g + s8], v << (16 * (c & 1)));
+        W.a4[c] = 0;
+    }
+}
+
+// A complex read (more than kPre CIGAR ops, more than 4 runs, or a huge span) walked by the
+// whole wave, 64 consecutive reference offsets per step, straight into the global counts.
+template <bool QUAL, int NC>
+__device__ void rc_complex(const RcArgs& A, int64_t r, int64_t& bad) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p0 = A.pos[r];
+    const uint32_t* cg = A.cigar + A.cig_beg[r];
+    const uint32_t cn = A.cig_n[r], sn = A.seq_nib[r];
+    uint64_t span = 0;
+    for (uint32_t k = 0; k < cn; ++k)
+        if (mlike(cg[k] & 15u) || dlike(cg[k] & 15u)) span += cg[k] >> 4;
+    for (uint64_t e0 = 0; e0 < span; e0 += 64) {
+        const uint64_t j = e0 + lane;
+        uint32_t e = kNone;
+        uint64_t rc = 0, qc = 0;
+        for (uint32_t k = 0; k < cn && rc < e0 + 64; ++k) {
+            const uint32_t op = cg[k] & 15u, len = cg[k] >> 4;
+            if (mlike(op) || dlike(op)) {
+                if (j >= rc && j < rc + len) e = mlike(op) ? (uint32_t)(sn + qc + (j - rc)) : kDel;
+                rc += len;
+            }
+            if (qcons(op)) qc += len;
+        }
+        if (e == kNone) continue;
+        unsigned col = 4;
+        bool ok = true;
+        if (e != kDel) {
+            col = nib_col6((A.seq[e >> 1] >> ((e & 1u) * 4)) & 15u);
+            ok = col != 6u;
+            if (QUAL) ok = ok && (uint32_t)A.qual[e] >= A.mbq;
+        }
+        if (!ok) continue;
+        const int64_t p = p0 + (int64_t)j;
+        if (p >= A.L) {
+            if (r < bad) bad = r;
+        } else if ((int)col < NC) {
+            atomicAdd(&A.counts[(int64_t)col * A.L + p], 1);
+        }
+    }
+}
+
+template <bool QUAL, int NC>
+__global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
+    __shared__ uint4 rec[kRcReads * 3];                                  // 12 KB
+    __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 32];  // + pads
+    __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
+    __shared__ uint32_t red[kRcWaves][8];
+    __shared__ uint32_t wlo[kRcWin], whi[kRcWin], wpre[kRcWin + 1];
+    __shared__ uint32_t cxl[kRcReads];
+    __shared__ uint32_t ncx;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, s8 = lane & 7;
+    uint8_t* stage = stage_raw + 16;
+    auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+    int64_t bad = INT64_MAX;
+
+    for (int64_t chunk = blockIdx.x; chunk < A.n_chunks; chunk += gridDim.x) {
+        const int64_t c0 = chunk * kRcReads;
+        const int nr = (int)(A.n - c0 < kRcReads ? A.n - c0 : kRcReads);
+        // ---- 1. setup: one read per thread
+        const bool valid = tid < nr;
+        uint32_t mpos = 0x7FFFFFFFu, msn = 0, mcb = 0, mcn = 0;
+        if (valid) {
+            mpos = (uint32_t)A.pos[c0 + tid];
+            mcb = A.cig_beg[c0 + tid];
+            mcn = A.cig_n[c0 + tid];
+            msn = A.seq_nib[c0 + tid];
+        }
+        RunTable T;
+        T.nrun = 0;
+        T.gap = T.complex = false;
+        T.span = T.qlen = 0;
+#pragma unroll
+        for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
+        const int cmax = (int)U(wave_reduce<true>(valid ? (mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre) : 0u));
+        if (valid) {
+            uint32_t w[kPre];
+#pragma unroll
+            for (int i = 0; i < kPre; ++i) {
+                w[i] = 0u;
+                if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
+            }
+            T = decode_runs(w, mcn, cmax);
+        }
+        const bool cx = valid && T.complex;
+        const bool simple = valid && !cx;
+        if (tid == 0) ncx = 0;
+        // chunk bounds: P0 / P1 over all reads (complex ones: their true span), sequence segment
+        // and maxima over the simple reads
+        uint32_t cspan = T.span;
+        if (cx) {
+            uint64_t sp = 0;
+            for (uint32_t k = 0; k < mcn; ++k) {
+                const uint32_t wk = A.cigar[mcb + k];
+                if (mlike(wk & 15u) || dlike(wk & 15u)) sp += wk >> 4;
+            }
+            cspan = sp > 0x3FFFFFFFu ? 0x3FFFFFFFu : (uint32_t)sp;
+        }
+        uint32_t v[7] = {valid ? mpos : 0xFFFFFFFFu,
+                         valid ? mpos + cspan : 0u,
+                         (simple && T.qlen) ? (msn >> 1) : 0xFFFFFFFFu,
+                         (simple && T.qlen) ? ((msn + T.qlen + 1) >> 1) : 0u,
+                         simple ? T.span : 0u,
+                         simple ? (uint32_t)T.nrun : 0u,
+                         (simple && T.gap) ? 1u : 0u};
+        const bool is_max[7] = {false, true, false, true, true, true, true};
+        block_reduce<7>(v, is_max, red);  // contains a __syncthreads
+        const int64_t P0 = v[0], P1 = v[1];
+        uint32_t seg_lo = v[2];
+        const uint32_t seg_hi = v[3];
+        const int maxspan = (int)v[4], maxrun = (int)v[5];
+        const bool gap = v[6] != 0;
+        seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
+        const bool staged = seg_hi - seg_lo <= (uint32_t)kStage;
+        if (cx) cxl[atomicAdd(&ncx, 1u)] = (uint32_t)tid;
+        // ---- stage the chunk's sequence (16 B per thread per pass)
+        if (staged) {
+            for (uint32_t off = tid * 16u; off < seg_hi - seg_lo; off += kRcThreads * 16u) {
+                uint4 q4 = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
+                if (QUAL) {
+                    const int64_t q0 = 2 * ((int64_t)seg_lo + off);
+                    uint32_t qw[8];
+                    if (((uintptr_t)A.qual & 15u) == 0 && q0 + 32 <= A.qual_bytes) {
+                        const uint4 qa = *(const uint4*)(A.qual + q0), qb = *(const uint4*)(A.qual + q0 + 16);
+                        qw[0] = qa.x, qw[1] = qa.y, qw[2] = qa.z, qw[3] = qa.w;
+                        qw[4] = qb.x, qw[5] = qb.y, qw[6] = qb.z, qw[7] = qb.w;
+                    } else {
+                        for (int i = 0; i < 8; ++i) {
+                            qw[i] = 0;
+                            for (int bb = 0; bb < 4; ++bb) {
+                                const int64_t at = q0 + 4 * i + bb;
+                                if (at < A.qual_bytes) qw[i] |= (uint32_t)A.qual[at] << (8 * bb);
+                            }
+                        }
+                    }
+                    q4.x &= qual_nibmask(qw[0], qw[1], A.mbq);
+                    q4.y &= qual_nibmask(qw[2], qw[3], A.mbq);
+                    q4.z &= qual_nibmask(qw[4], qw[5], A.mbq);
+                    q4.w &= qual_nibmask(qw[6], qw[7], A.mbq);
+                }
+                *(uint4*)(stage + off) = q4;
+            }
+        }
+        // ---- records (pos kept for complex / padding entries so pos[] stays sorted)
+        {
+            const uint32_t qbase = staged ? 2u * seg_lo : 0u;
+            uint32_t rr[kMaxRuns], nb[kMaxRuns];
+#pragma unroll
+            for (int k = 0; k < kMaxRuns; ++k) {
+                rr[k] = simple ? pack_rr(T.st[k], T.en[k]) : 0u;
+                nb[k] = msn - qbase + (uint32_t)T.qd[k];
+            }
+            rec[tid * 3] = make_uint4(mpos, simple ? T.span * 4u : 0u, rr[0], nb[0]);
+            rec[tid * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
+            rec[tid * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
+        }
+        __syncthreads();  // stage, records and the complex-read list complete
+        const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
+                         staged ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
+        const int64_t WB = P0 & ~(int64_t)7;
+        const int64_t NW = P1 > WB ? (P1 - WB + 7) / 8 : 0;
+        // ---- 2./3. window passes of up to kRcWin windows
+        for (int64_t wp = 0; wp < NW; wp += kRcWin) {
+            const int nwin = (int)(NW - wp < kRcWin ? NW - wp : kRcWin);
+            const int64_t PB = WB + 8 * wp;
+            for (int t = tid; t < 3 * kRcWinPos; t += kRcThreads) (&hist[0][0])[t] = 0u;
+            if (wave == 0) {
+                // reads overlapping window t: pos in [gb - maxspan + 1, gb + 8) (sorted records)
+                uint32_t cnt = 0;
+                if (lane < nwin) {
+                    const int64_t gb = PB + 8 * lane;
+                    const int64_t lo_key = gb - maxspan + 1, hi_key = gb + 8;
+                    uint32_t a = 0, b = 0;
+                    for (uint32_t step = kRcReads; step; step >>= 1) {  // branch-free lower bounds
+                        if (a + step <= (uint32_t)nr && (int64_t)rec[(a + step - 1) * 3].x < lo_key) a += step;
+                        if (b + step <= (uint32_t)nr && (int64_t)rec[(b + step - 1) * 3].x < hi_key) b += step;
+                    }
+                    wlo[lane] = a;
+                    whi[lane] = b;
+                    cnt = b > a ? (b - a + 63) / 64 : 0u;
+                }
+                // exclusive prefix of the item counts over the windows (DPP scan)
+                uint32_t inc = cnt;
+                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x111, 0xF, 0xF, false);
+                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x112, 0xF, 0xF, false);
+                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x114, 0xF, 0xF, false);
+                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x118, 0xF, 0xF, false);
+                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x142, 0xA, 0xF, false);
+                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x143, 0xC, 0xF, false);
+                if (lane < nwin) wpre[lane] = inc - cnt;
+                if (lane == nwin - 1) wpre[nwin] = inc;
+            }
+            __syncthreads();  // hist zeroed, window table ready
+            // this wave's items [k0, k1): contiguous, so it changes window only a few times
+            const uint32_t I = U(wpre[nwin]);
+            const uint32_t k0 = (uint32_t)(((uint64_t)I * wave) / kRcWaves);
+            const uint32_t k1 = (uint32_t)(((uint64_t)I * (wave + 1)) / kRcWaves);
+            Swar W;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) W.a4[c] = 0;
+            int g = 0, it4 = 0;
+            while (g + 1 < nwin && U(wpre[g + 1]) <= k0) ++g;
+            uint32_t gnext = U(wpre[g + 1]), gpre = U(wpre[g]), glo = U(wlo[g]), ghi = U(whi[g]);
+            for (uint32_t k = k0; k < k1; ++k) {
+                if (k >= gnext) {  // next window (wave-uniform)
+                    if (it4) rc_fold<NC>(W, hist, g, s8);
+                    it4 = 0;
+                    while (k >= U(wpre[g + 1])) ++g;
+                    gnext = U(wpre[g + 1]);
+                    gpre = U(wpre[g]);
+                    glo = U(wlo[g]);
+                    ghi = U(whi[g]);
+                }
+                const int gb = (int)(PB + 8 * g);
+                const uint32_t r = glo + 64u * (k - gpre) + (uint32_t)lane;
+                const bool in = r < ghi;
+                const int rs = in ? (int)r : 0;
+                uint32_t x;
+                if (maxrun <= 1) {
+                    x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
+                                      : window_events<1, true, false, QUAL>(src, rec, rs, gb))
+                            : (staged ? window_events<1, false, true, QUAL>(src, rec, rs, gb)
+                                      : window_events<1, false, false, QUAL>(src, rec, rs, gb));
+                } else if (maxrun == 2) {
+                    x = staged ? window_events<2, true, true, QUAL>(src, rec, rs, gb)
+                               : window_events<2, true, false, QUAL>(src, rec, rs, gb);
+                } else {
+                    x = staged ? window_events<4, true, true, QUAL>(src, rec, rs, gb)
+                               : window_events<4, true, false, QUAL>(src, rec, rs, gb);
+                }
+                x = in ? x : 0u;
+                if ((int64_t)gb + 8 > A.L) {  // window reaches past the reference end
+                    int64_t kL = A.L - gb;
+                    kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
+                    const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
+                    if ((x & bmask) && c0 + (int64_t)r < bad) bad = c0 + (int64_t)r;
+                    x &= ~bmask;
+                }
+                swar_add<NC>(W, x);
+                if (++it4 == 14) {
+                    rc_fold<NC>(W, hist, g, s8);
+                    it4 = 0;
+                }
+            }
+            if (it4) rc_fold<NC>(W, hist, g, s8);
+            __syncthreads();
+            // ---- 4. flush the pass's positions (< L) into the counts
+            for (int t = tid; t < 8 * nwin; t += kRcThreads) {
+                const int64_t p = PB + t;
+                if (p >= A.L) break;
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) {
+                    const uint32_t hv = hist[pl][t];
+                    const uint32_t lo = hv & 0xFFFFu, hi = hv >> 16;
+                    if (lo && 2 * pl < NC) atomicAdd(&A.counts[(int64_t)(2 * pl) * A.L + p], (int32_t)lo);
+                    if (hi && 2 * pl + 1 < NC) atomicAdd(&A.counts[(int64_t)(2 * pl + 1) * A.L + p], (int32_t)hi);
+                }
+            }
+            __syncthreads();  // hist reused by the next pass / chunk
+        }
+        // ---- complex reads: one wave per read, global atomics
+        const uint32_t nc = U(ncx);
+        for (uint32_t q = wave; q < nc; q += kRcWaves) rc_complex<QUAL, NC>(A, c0 + cxl[q], bad);
+        __syncthreads();  // records / stage / cxl reused by the next chunk
+    }
+    // first offending read of this block (std::out_of_range in the reference)
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t b2 = __shfl_down(bad, o);
+        bad = b2 < bad ? b2 : bad;
+    }
+    if (lane == 0 && bad != INT64_MAX) atomicMin(A.err, (unsigned long long)bad);
+}
+
+}  // namespace
+
+bool use_rc(const bc_reads& r, int64_t L) {
+    if (!r.sorted || r.n_reads <= 0 || r.seq_layout != BC_SEQ_EVENT) return false;
+    if (const char* e = std::getenv("BC_PILEUP_PATH")) {
+        if (!std::strcmp(e, "rc")) return true;
+        if (!std::strcmp(e, "tile")) return r.max_span > kTileMaxSpan;
+    }
+    if (r.max_span > kTileMaxSpan) return true;  // the tiled kernel's look-back gets too long
+    const int64_t reach = r.max_end > L ? r.max_end : L;
+    const double per_tile = reach > 0 ? (double)r.n_reads * (double)(r.max_span + 63) / (double)reach : 0.0;
+    return per_tile >= kRcMinReadsPerTile;
+}
+
+hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, int ncols, int32_t* counts,
+                     unsigned long long* d_err) {
+    if (r.n_reads <= 0) return hipSuccess;
+    RcArgs A;
+    A.pos = r.pos;
+    A.cig_beg = r.cig_beg;
+    A.cig_n = r.cig_n;
+    A.seq_nib = r.seq_nib;
+    A.cigar = r.cigar;
+    A.seq = r.seq;
+    A.qual = r.qual;
+    A.n = r.n_reads;
+    A.L = L;
+    A.mbq = mbq;
+    A.seq_words = (int64_t)(seq_event_bytes(r.seq_bytes) / 4);
+    A.qual_bytes = r.qual ? r.qual_bytes : 0;
+    A.n_chunks = (r.n_reads + kRcReads - 1) / kRcReads;
+    A.counts = counts;
+    A.err = d_err;
+    int64_t blocks = A.n_chunks < 256 * 4 ? A.n_chunks : 256 * 4;
+    const dim3 grid((unsigned)blocks), block(kRcThreads);
+    if (mbq > 0) {
+        if (ncols == 6) hipLaunchKernelGGL((k_rc<true, 6>), grid, block, 0, s, A);
+        else hipLaunchKernelGGL((k_rc<true, 5>), grid, block, 0, s, A);
+    } else {
+        if (ncols == 6) hipLaunchKernelGGL((k_rc<false, 6>), grid, block, 0, s, A);
+        else hipLaunchKernelGGL((k_rc<false, 5>), grid, block, 0, s, A);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace bc

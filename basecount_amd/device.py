@@ -16,7 +16,7 @@ from ._native import _libs, _load
 
 BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV = -1, -2, -3, -4
 BC_SEQ_BAM, BC_SEQ_EVENT = 0, 1
-KERNEL_NAMES = ("count", "stats", "reserved", "pileup", "summary", "amplicons")  # BC_K_* ids
+KERNEL_NAMES = ("count", "stats", "rc", "pileup", "summary", "amplicons")  # BC_K_* ids
 KERNEL_IDS = len(KERNEL_NAMES)
 
 

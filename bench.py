@@ -32,16 +32,22 @@ WORKLOADS = {
 }
 
 
-def pileup_bytes(b: dict, L: int, k: int, mbq: int, l_seq: np.ndarray, with_pc: bool = True) -> int:
-    """Algorithmic HBM bytes of one fused k_pileup launch (roofline): per read 16 B of
-    read index (pos, cig_beg, cig_n, seq_nib) + 4 B per CIGAR word + ceil(l_seq/2) B of packed
-    SEQ (+ l_seq B of QUAL when mbq > 0); per position the outputs written once: k int32 counts,
-    int32 coverage, k f64 percentages (when requested), f64 entropy and secondary entropy."""
+def read_bytes(b: dict, mbq: int, l_seq: np.ndarray) -> int:
+    """Algorithmic bytes of the read batch (roofline): per read 16 B of read index
+    (pos, cig_beg, cig_n, seq_nib) + 4 B per CIGAR word + ceil(l_seq/2) B of packed SEQ (+ l_seq
+    B of QUAL when mbq > 0)."""
     n = int(b["pos"].size)
-    per_read = 16 * n + 4 * int(b["cig_n"].sum()) + int(((l_seq + 1) // 2).sum())
-    if mbq > 0:
-        per_read += int(l_seq.sum())
-    return per_read + L * (4 * k + 4 + (8 * k if with_pc else 0) + 16)
+    nb = 16 * n + 4 * int(b["cig_n"].sum()) + int(((l_seq + 1) // 2).sum())
+    return nb + (int(l_seq.sum()) if mbq > 0 else 0)
+
+
+def kernel_bytes(kernel: str, rb: int, L: int, k: int, with_pc: bool = True) -> int:
+    """Algorithmic HBM bytes of one launch: the fused k_pileup reads the batch and writes per
+    position k int32 counts, int32 coverage, k f64 percentages (when requested) and two f64
+    entropies; k_rc reads the batch and writes the counts; k_stats reads the counts and writes
+    the statistics."""
+    stats_out = L * (4 + (8 * k if with_pc else 0) + 16)
+    return {"pileup": rb + 4 * k * L + stats_out, "rc": rb + 4 * k * L, "stats": 4 * k * L + stats_out}[kernel]
 
 
 def cpu_baseline(rs, b, L: int, budget_s: float = 10.0) -> dict:
@@ -157,19 +163,39 @@ def main():
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    k1 = ctx.event_elapsed_ms(0, 1) * 1e-3 / args.steps  # s per step on the device (one launch)
+    dev_step = ctx.event_elapsed_ms(0, 1) * 1e-3 / args.steps  # s per step on the device
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # ---- per-launch hipEvent pairs (library timing facility; includes event overhead) --------
+    # ---- which kernels a step launches (library timing facility, per-launch event pairs) -------
     ctx.timing(True)
-    for _ in range(min(args.steps, 50)):
-        step()
-    rep = ctx.timing_report()
+    step()
+    launched = [name for name in ctx.timing_report()]
     ctx.timing(False)
-    k1_pair = rep["pileup"][1] * 1e-6
+
+    def region(fn, reps):  # on-device seconds per call: hipEvents around `reps` back-to-back calls
+        ctx.sync()
+        ctx.event_record(2)
+        for _ in range(reps):
+            fn()
+        ctx.event_record(3)
+        return ctx.event_elapsed_ms(2, 3) * 1e-3 / reps
+
+    # per-kernel average durations, each timed as a region of back-to-back launches of that
+    # kernel alone (a one-kernel step: the step region itself)
+    kern_s = {}
+    if launched == ["pileup"]:
+        kern_s["pileup"] = dev_step
+    else:  # deep batch: memset + k_rc + k_stats (bc_count on the same batch launches k_rc alone)
+        reps = max(5, min(args.steps, 50))
+        kern_s["rc"] = region(lambda: ctx.count(reads, L, args.mbq, k, counts.ptr), reps)
+        kern_s["stats"] = region(lambda: ctx.stats(counts.ptr, L, k, nf, nf2, dcov.ptr, dpc.ptr, dent.ptr,
+                                                   dsec.ptr), reps)
+        step()  # restore the step's outputs (the count-only regions accumulated into `counts`)
+        ctx.sync()
+    dom = max(kern_s, key=kern_s.get)
 
     # ---- correctness of what was timed (rank-local): counts vs the oracle -------------------
     got = counts.download(np.int32, ncols * L).reshape(ncols, L)
@@ -194,14 +220,17 @@ def main():
     events = synth.ref_events(rs)
     ms = elapsed / args.steps * 1e3
     positions = world * L * args.steps
-    kbytes = pileup_bytes(b, L, k, args.mbq, rs.l_seq)
-    achieved = kbytes / k1 / 1e9
+    rb = read_bytes(b, args.mbq, rs.l_seq)
+    kbytes = kernel_bytes(dom, rb, L, k)
+    achieved = kbytes / kern_s[dom] / 1e9
+    kernel_names = {"pileup": "k_pileup (fused kernel 1 + 2)", "rc": "k_rc (read-chunked kernel 1)",
+                    "stats": "k_stats (kernel 2)"}
     traffic = None
     pmc = os.path.join(REPO, "profiles", "kernel1_pmc.json")
     if os.path.exists(pmc):
         with open(pmc) as fh:
             pm = json.load(fh).get(args.config, {})
-        if pm and pm.get("mbq", 0) == args.mbq:
+        if pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom:
             traffic = pm.get("hbm_bytes_per_launch")
 
     if rank == 0:
@@ -226,13 +255,14 @@ def main():
                        "positions_per_rank": L, "min_base_quality": args.mbq,
                        "parallelism": f"contig-sharded x{world}"},
             "gbases_piled_per_s": world * events * args.steps / elapsed / 1e9,
-            "pileup_kernel_us": k1 * 1e6,
-            "pileup_kernel_us_event_pair": k1_pair * 1e6,
-            "kernels": "k_pileup (kernel 1 and kernel 2 fused, one launch per step), eager launches",
+            "device_us_per_step": dev_step * 1e6,
+            "kernel_us": {kernel_names[n]: v * 1e6 for n, v in kern_s.items()},
+            "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per step" if dom == "pileup"
+                        else "memset + k_rc (kernel 1) + k_stats (kernel 2) per step") + ", eager launches",
             "parity_vs_oracle": parity,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_pileup (fused kernel 1 + 2)", "algorithmic_bytes": kbytes},
+                         "kernel": kernel_names[dom], "algorithmic_bytes": kbytes},
             "cpu_baseline": cpu,
             "gather_ms": gather_ms,
         }

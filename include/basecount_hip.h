@@ -155,7 +155,7 @@ int bc_graph_destroy(bc_graph* g);
  * the record.  Do not enable while capturing a graph.                                          */
 #define BC_K_COUNT 0      /* event-parallel kernel 1 (unsorted / long-span batches) */
 #define BC_K_STATS 1      /* kernel 2                                              */
-#define BC_K_RESERVED 2   /* (unused)                                              */
+#define BC_K_RC 2         /* read-chunked kernel 1 (deep sorted batches)           */
 #define BC_K_PILEUP 3     /* fused tiled kernel 1 + 2                              */
 #define BC_K_SUMMARY 4
 #define BC_K_AMPLICONS 5

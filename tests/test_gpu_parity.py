@@ -91,7 +91,11 @@ def random_batch(rng, L, n, long_skip=False, sort=True, nfrac=0.05):
     (4, 50_000, 3_000, True, True), (5, 300, 4_000, True, False), (6, 1_000_000, 2_000, True, False),
 ])
 @pytest.mark.parametrize("mbq", [0, 20, 40])
-def test_kernel1_matches_oracle(ctx, seed, L, n, sort, long_skip, mbq):
+@pytest.mark.parametrize("path", ["tile", "rc"])
+def test_kernel1_matches_oracle(ctx, monkeypatch, seed, L, n, sort, long_skip, mbq, path):
+    """Sorted batches take the tiled (k_pileup) or the read-chunked (k_rc) kernel, unsorted
+    ones the event-parallel k_count: identical counts."""
+    monkeypatch.setenv("BC_PILEUP_PATH", path)
     rng = np.random.default_rng(seed)
     b = random_batch(rng, L, n, long_skip=long_skip, sort=sort)
     exp, (br, _) = O.bcount(L, mbq, b)
@@ -156,7 +160,9 @@ def gpu_pileup(ctx, b, L, mbq, k):
 @pytest.mark.parametrize("seed,L,n", [(11, 700, 900), (12, 29_903, 30_000), (13, 5_000, 60_000),
                                       (14, 2_000_000, 3_000), (15, 64, 50), (16, 65, 80)])
 @pytest.mark.parametrize("mbq,show_n", [(0, False), (20, True), (40, False)])
-def test_fused_pileup_matches_oracle(ctx, seed, L, n, mbq, show_n):
+@pytest.mark.parametrize("path", ["tile", "rc"])
+def test_fused_pileup_matches_oracle(ctx, monkeypatch, seed, L, n, mbq, show_n, path):
+    monkeypatch.setenv("BC_PILEUP_PATH", path)
     rng = np.random.default_rng(seed)
     b = random_batch(rng, L, n)
     k = 6 if show_n else 5
@@ -170,7 +176,9 @@ def test_fused_pileup_matches_oracle(ctx, seed, L, n, mbq, show_n):
     assert np.max(np.abs(ent - oent)) <= 1e-6 and np.max(np.abs(sec - osec)) <= 1e-6
 
 
-def test_fused_pileup_range_error(ctx):
+@pytest.mark.parametrize("path", ["tile", "rc"])
+def test_fused_pileup_range_error(ctx, monkeypatch, path):
+    monkeypatch.setenv("BC_PILEUP_PATH", path)
     rng = np.random.default_rng(21)
     b = random_batch(rng, 2_000, 3_000)
     for L2 in (1_990, 1_900, 1_000, 64):
@@ -338,7 +346,9 @@ def test_bcount_adapter_matches_reference_vectors(golden):
 
 # ------------------------------------------------------------------ full-size configurations
 @pytest.mark.parametrize("cfg,mmq,mbq", [("c2", 0, 0), ("c3", 0, 0), ("c3", 30, 20)])
-def test_full_size_configs_exact(ctx, cfg, mmq, mbq):
+@pytest.mark.parametrize("path", ["tile", "rc"])
+def test_full_size_configs_exact(ctx, monkeypatch, cfg, mmq, mbq, path):
+    monkeypatch.setenv("BC_PILEUP_PATH", path)
     rs = synth.make_config(cfg)
     b = synth.batch_arrays(rs, 0, mmq)
     L = rs.lengths[0]
@@ -348,3 +358,20 @@ def test_full_size_configs_exact(ctx, cfg, mmq, mbq):
     assert np.array_equal(got, exp[:, :5].T.astype(np.int32))
     if mbq == 0 and mmq == 0:  # every ref-consuming event is counted: checksum of checksums
         assert int(got.sum()) + int(exp[:, 5].sum()) == synth.ref_events(rs)
+
+
+@pytest.mark.parametrize("path", ["auto", "tile", "rc"])
+def test_full_size_c3_fused_pileup(ctx, monkeypatch, path):
+    """The bench's step (bc_pileup) on the full C3 batch: counts exact, stats within 1e-6."""
+    if path != "auto":
+        monkeypatch.setenv("BC_PILEUP_PATH", path)
+    rs = synth.make_config("c3")
+    b = synth.batch_arrays(rs, 0, 0)
+    L = rs.lengths[0]
+    exp, (br, _) = O.bcount(L, 0, b)
+    (cnt, cov, pc, ent, sec), bad = gpu_pileup(ctx, b, L, 0, 5)
+    assert br == -1 and bad == -1
+    assert np.array_equal(cnt, exp[:, :5].T.astype(np.int32))
+    ocov, opc, oent, osec = O.stats(exp, False)
+    assert np.array_equal(cov, ocov) and np.array_equal(pc, opc)
+    assert np.max(np.abs(ent - oent)) <= 1e-6 and np.max(np.abs(sec - osec)) <= 1e-6

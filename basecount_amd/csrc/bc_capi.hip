@@ -357,8 +357,6 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
     if (k != 5 && k != 6) return fail(BC_E_ARG, "k must be 5 or 6");
     if (L < 0) return fail(BC_E_ARG, "ref_len < 0");
     if (!r->sorted) return fail(BC_E_ARG, "bc_pileup needs a coordinate-sorted batch (sorted == 1)");
-    if (r->max_span > bc::kTileMaxSpan)
-        return fail(BC_E_ARG, "bc_pileup: max_span above 4096; use bc_count + bc_stats");
     if (mbq > 0 && r->n_reads > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
     if (r->n_reads > 0 && r->seq_layout != BC_SEQ_EVENT)
         return fail(BC_E_ARG, "bc_pileup needs seq_layout == BC_SEQ_EVENT (see bc_seq_to_event)");

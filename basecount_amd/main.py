@@ -22,6 +22,7 @@ replayed from the fault positions (``_first_error``).
 from __future__ import annotations
 
 import argparse
+import json
 import ctypes as C
 import math
 import os
@@ -50,10 +51,12 @@ _CONTEXTS: dict = {}
 
 
 def default_device() -> int:
-    for var in ("BASECOUNT_DEVICE", "LOCAL_RANK"):
-        v = os.environ.get(var)
-        if v not in (None, ""):
-            return int(v)
+    v = os.environ.get("BASECOUNT_DEVICE")
+    if v not in (None, ""):
+        return int(v)
+    v = os.environ.get("LOCAL_RANK")
+    if v not in (None, ""):  # one process per GPU; ranks beyond the GPU count share devices
+        return int(v) % max(1, D.device_count())
     return 0
 
 
@@ -368,10 +371,14 @@ class _FileOnDevice:
 
 def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality=0,
                    chunk_size=1000000, show_n_bases=False, long_format=False, *, device=None,
-                   _mode="rows", _tiles=None):
+                   _mode="rows", _tiles=None, _group=None):
     """main.py:110-205 on the device.  Returns {ref: {"rows": Rows, "num_reads": n}} in the
     reference's (set) order.  ``_mode="summary"`` keeps per-position data in HBM and returns
-    the numpy-exact summary (and amplicon) reductions instead of rows."""
+    the numpy-exact summary (and amplicon) reductions instead of rows.
+
+    With ``_group`` (a dist.Group, one process per GPU) the references are sharded over the
+    ranks (dist.shard): this rank computes and returns only the ones it owns, and the function
+    returns ``(results, owner, order)``; every rank raises the same first error."""
     samfile = open_samfile(bam)
     try:
         references = get_references(samfile, references)
@@ -391,23 +398,38 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
             m = (rec_err[b0:b1] & _TYPE_FAULTS) != 0
             type_ord[ref] = int(sel.ordinal[b0 + int(np.argmax(m))]) if m.any() else -1
 
+        nreads = {ref: int(sel.ref_beg[ref_index[ref] + 1] - sel.ref_beg[ref_index[ref]])
+                  for ref in ref_order}
+        owner = None
+        mine = ref_order
+        if _group is not None:
+            from .dist import shard
+
+            # cost estimate: per-position outputs + per-read work (both linear)
+            owner = shard(ref_order, {r: int(reference_lengths[r]) + 100 * nreads[r] for r in ref_order},
+                          _group.world)
+            mine = [r for r in ref_order if owner[r] == _group.rank]
         results, range_idx = {}, {}
-        if 0 <= mbq < _U32:
+        if 0 <= mbq < _U32 and mine:
             ctx = context(device)
             fod = _FileOnDevice(ctx, samfile, sel, need_qual=mbq > 0)
             nf, nf2 = norm_factors(k)
-            for ref in ref_order:
+            for ref in mine:
                 t = ref_index[ref]
                 L = int(reference_lengths[ref])
                 results[ref], range_idx[ref] = _device_reference(
                     ctx, fod.reads(t), L, mbq, ncols, k, nf, nf2, _mode,
                     _tiles(ref) if _tiles else None, _tiles is not None)
+        if _group is not None and 0 <= mbq < _U32:
+            # every rank needs every reference's first out-of-range read to raise the same error
+            alls = _group.all_gather_ints([range_idx.get(r, -2) for r in ref_order])
+            range_idx = {r: alls[owner[r]][i] for i, r in enumerate(ref_order)}
         err = _first_error(samfile, sel, ref_order, ref_index, reference_lengths, mbq,
                            int(chunk_size), type_ord, range_idx)
         if err is not None:
             raise err
         out = {}
-        for ref in ref_order:
+        for ref in mine:
             t = ref_index[ref]
             n = int(sel.ref_beg[t + 1] - sel.ref_beg[t])
             if _mode == "rows":
@@ -415,6 +437,8 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
             else:
                 out[ref] = {"summary": results[ref], "num_reads": n,
                             "length": int(reference_lengths[ref])}
+        if _group is not None:
+            return out, owner, ref_order
         return out
     finally:
         samfile.close()
@@ -437,7 +461,7 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
     outs = _alloc_outputs(ctx, k, L, want_pc=(mode == "rows"))
     hist = ctx.alloc(4 * ncols * L)
     pc_ptr = outs["pc"].ptr if outs["pc"] else None
-    if reads.sorted and reads.max_span <= 4096:
+    if reads.sorted:
         ctx.pileup(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
                    outs["sec"].ptr)
     else:
@@ -477,16 +501,7 @@ class BaseCount:
     def __init__(self, bam, references=None, min_base_quality=0, min_mapping_quality=0,
                  chunk_size=1000000, show_n_bases=False, long_format=False, *, device=None,
                  _mode="rows", _tiles=None):
-        if long_format:
-            self.columns = ["reference", "position", "coverage", "base", "count", "percentage",
-                            "entropy", "secondary_entropy"]
-        else:
-            self.columns = ["reference", "position", "coverage", "num_a", "num_c", "num_g",
-                            "num_t", "num_ds", "num_n", "pc_a", "pc_c", "pc_g", "pc_t", "pc_ds",
-                            "pc_n", "entropy", "secondary_entropy"]
-            if not show_n_bases:
-                self.columns.pop(self.columns.index("num_n"))
-                self.columns.pop(self.columns.index("pc_n"))
+        self.columns = _columns(show_n_bases, long_format)
         self.data = get_basecounts(bam, references=references, min_base_quality=min_base_quality,
                                    min_mapping_quality=min_mapping_quality, chunk_size=chunk_size,
                                    show_n_bases=show_n_bases, long_format=long_format,
@@ -597,8 +612,58 @@ def _np_round_str(x, dp):
     return str(round(x, dp))
 
 
+def _columns(show_n_bases: bool, long_format: bool) -> list:
+    """main.py:233-264."""
+    if long_format:
+        return ["reference", "position", "coverage", "base", "count", "percentage", "entropy",
+                "secondary_entropy"]
+    cols = ["reference", "position", "coverage", "num_a", "num_c", "num_g", "num_t", "num_ds",
+            "num_n", "pc_a", "pc_c", "pc_g", "pc_t", "pc_ds", "pc_n", "entropy", "secondary_entropy"]
+    if not show_n_bases:
+        cols.pop(cols.index("num_n"))
+        cols.pop(cols.index("pc_n"))
+    return cols
+
+
+_AMP_NAMES = ["mean_coverage_amplicon_vector", "median_coverage_amplicon_vector",
+              "mean_entropy_amplicon_vector", "median_entropy_amplicon_vector",
+              "mean_secondary_entropy_amplicon_vector", "median_secondary_entropy_amplicon_vector"]
+
+
+def _print_summary(ref, s, ref_length, num_reads, dp, bed, bed_error):
+    """main.py:469-595 for one reference (summary lines, then the amplicon vectors)."""
+    if ref_length == 0:
+        np.mean([])  # the reference's RuntimeWarning, then its ZeroDivisionError
+        raise ZeroDivisionError("division by zero")
+    pc_ref_coverage = 100 * (s["nnz"] / ref_length)
+    summary_stats = {
+        "reference_name": ref,
+        "reference_length": round(ref_length, dp),
+        "num_reads": round(num_reads, dp),
+        "pc_reference_coverage": round(pc_ref_coverage, dp),
+        "avg_depth": round(s["avg_cov"], dp),
+        "avg_entropy": round(s["avg_ent"], dp),
+    }
+    for name, val in summary_stats.items():
+        print(name, val, sep="\t")
+    if bed is not None:
+        if bed_error is not None:
+            raise bed_error
+        amp, empty = s["amplicons"]
+        vecs = [[] for _ in range(6)]
+        for i, e in enumerate(empty):
+            for j in range(6):
+                vecs[j].append(-1 if e else np.float64(amp[i, j]))
+        for name, vec in zip(_AMP_NAMES, vecs):
+            val = ", ".join([_np_round_str(x, dp) for x in vec]) if vec else "-"
+            print(name, val, sep="\t")
+
+
 def run(argv=None):
-    """main.py:378-595: `basecount BAM [--long-format | --summarise | --summarise-with-bed BED]`."""
+    """main.py:378-595: `basecount BAM [--long-format | --summarise | --summarise-with-bed BED]`.
+
+    Under torchrun (WORLD_SIZE > 1) the references are sharded over the ranks (dist.py); the
+    output is identical to a single process's."""
     args = build_parser().parse_args(argv)
     references = handle_arg(args.references, "references")
     min_base_quality = int(handle_arg(args.min_base_quality, "min-base-quality", default=0,
@@ -610,17 +675,43 @@ def run(argv=None):
     bed = handle_arg(args.summarise_with_bed, "bed", provided_once=True)
     decimal_places = int(handle_arg(args.decimal_places, "decimal_places", default=3,
                                     provided_once=True))
+    from . import dist
 
+    group = dist.Group() if dist.env()[0] > 1 else None  # before the HIP library
+    try:
+        _run(args, references, min_base_quality, min_mapping_quality, chunk_size, bed,
+             decimal_places, group)
+    finally:
+        if group is not None:
+            group.close()
+
+
+def _run(args, references, min_base_quality, min_mapping_quality, chunk_size, bed, dp, group):
+    from . import dist
+
+    kw = dict(references=references, min_base_quality=min_base_quality,
+              min_mapping_quality=min_mapping_quality, chunk_size=chunk_size,
+              show_n_bases=args.show_n_bases, long_format=args.long_format)
     if (not args.summarise) and (bed is None):
-        bc = BaseCount(args.bam, references=references, min_base_quality=min_base_quality,
-                       min_mapping_quality=min_mapping_quality, chunk_size=chunk_size,
-                       show_n_bases=args.show_n_bases, long_format=args.long_format)
-        print("\t".join(bc.columns))
-        for ref in bc.references:
-            rows = bc.data[ref]["rows"]
+        if group is None:
+            bc = BaseCount(args.bam, **kw)
+            print("\t".join(bc.columns))
+            for ref in bc.references:
+                rows = bc.data[ref]["rows"]
+                d = rows.d
+                fmt.write_bytes(fmt.rows_text(ref, d.counts[: rows.k], d.pc, d.ent, d.sec, dp,
+                                              rows.long))
+            return
+        out, owner, order = get_basecounts(args.bam, **kw, _group=group)
+        if group.rank == 0:
+            print("\t".join(_columns(args.show_n_bases, args.long_format)), flush=True)
+        group.barrier()
+        blocks = {}
+        for ref, v in out.items():
+            rows = v["rows"]
             d = rows.d
-            fmt.write_bytes(fmt.rows_text(ref, d.counts[: rows.k], d.pc, d.ent, d.sec,
-                                          decimal_places, rows.long))
+            blocks[ref] = fmt.rows_text(ref, d.counts[: rows.k], d.pc, d.ent, d.sec, dp, rows.long)
+        dist.ordered_write(group, order, owner, blocks, write=fmt.write_bytes)
         return
 
     bed_errors = {}
@@ -635,43 +726,42 @@ def run(argv=None):
             return None
         return [(t[2]["inside_start"], t[2]["inside_end"]) for t in scheme]
 
-    bc = BaseCount(args.bam, references=references, min_base_quality=min_base_quality,
-                   min_mapping_quality=min_mapping_quality, chunk_size=chunk_size,
-                   show_n_bases=args.show_n_bases, long_format=args.long_format,
-                   _mode="summary", _tiles=tiles if bed is not None else None)
-    dp = decimal_places
-    for ref in bc.references:
-        s = bc.data[ref]["summary"]
-        ref_length = bc.reference_lengths[ref]
-        if ref_length == 0:
-            np.mean([])  # the reference's RuntimeWarning, then its ZeroDivisionError
-            raise ZeroDivisionError("division by zero")
-        pc_ref_coverage = 100 * (s["nnz"] / ref_length)
-        summary_stats = {
-            "reference_name": ref,
-            "reference_length": round(ref_length, dp),
-            "num_reads": round(bc.num_reads(ref), dp),
-            "pc_reference_coverage": round(pc_ref_coverage, dp),
-            "avg_depth": round(s["avg_cov"], dp),
-            "avg_entropy": round(s["avg_ent"], dp),
-        }
-        for name, val in summary_stats.items():
-            print(name, val, sep="\t")
-        if bed is not None:
-            if ref in bed_errors:
-                raise bed_errors[ref]
-            amp, empty = s["amplicons"]
-            vecs = [[] for _ in range(6)]
-            for i, e in enumerate(empty):
-                for j in range(6):
-                    vecs[j].append(-1 if e else np.float64(amp[i, j]))
-            names = ["mean_coverage_amplicon_vector", "median_coverage_amplicon_vector",
-                     "mean_entropy_amplicon_vector", "median_entropy_amplicon_vector",
-                     "mean_secondary_entropy_amplicon_vector",
-                     "median_secondary_entropy_amplicon_vector"]
-            for name, vec in zip(names, vecs):
-                val = ", ".join([_np_round_str(x, dp) for x in vec]) if vec else "-"
-                print(name, val, sep="\t")
+    tk = dict(_mode="summary", _tiles=tiles if bed is not None else None)
+    if group is None:
+        bc = BaseCount(args.bam, **kw, **tk)
+        for ref in bc.references:
+            _print_summary(ref, bc.data[ref]["summary"], bc.reference_lengths[ref], bc.num_reads(ref),
+                           dp, bed, bed_errors.get(ref))
+        return
+    # one process per GPU: exact numbers of the owned references gathered to rank 0 (float
+    # repr round-trips), printed there in the reference's order
+    out, owner, order = get_basecounts(args.bam, **kw, **tk, _group=group)
+    payload = {}
+    for ref, v in out.items():
+        s = v["summary"]
+        e = {"L": v["length"], "n": v["num_reads"]}
+        if v["length"]:
+            e.update(avg_cov=float(s["avg_cov"]), avg_ent=float(s["avg_ent"]), nnz=int(s["nnz"]))
+            if "amplicons" in s:
+                amp, empty = s["amplicons"]
+                e.update(amp=np.asarray(amp, np.float64).tolist(), empty=[bool(x) for x in empty])
+        payload[ref] = e
+    parts = group.gather_bytes(json.dumps(payload).encode())
+    if group.rank != 0:
+        return
+    merged = {}
+    for part in parts:
+        merged.update(json.loads(part.decode()))
+    for ref in order:
+        e = merged[ref]
+        s = {}
+        if e["L"]:
+            s = {"avg_cov": np.float64(e["avg_cov"]), "avg_ent": np.float64(e["avg_ent"]), "nnz": e["nnz"]}
+            if "amp" in e:
+                s["amplicons"] = (np.asarray(e["amp"], np.float64).reshape(-1, 6), e["empty"])
+        if bed is not None and owner[ref] != 0:
+            tiles(ref)  # the BED errors of references computed elsewhere, evaluated here
+        _print_summary(ref, s, e["L"], e["n"], dp, bed, bed_errors.get(ref))
 
 
 if __name__ == "__main__":

@@ -128,12 +128,15 @@ int bc_count(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min
              int ncols, int32_t* d_hist);
 
 /* Fused kernel 1 + kernel 2 — the hot path in ONE launch.  For a coordinate-sorted batch
- * (d_reads->sorted == 1, max_span <= 4096, max_end truthful) the reference is cut into
+ * (d_reads->sorted == 1, max_span / max_end truthful) the reference is cut into
  * 64-position tiles; each tile finds its reads by a search over pos[], walks them with lanes
  * owning 8-position windows and SWAR register counters (no atomics, no histogram memset;
  * needs seq_layout == BC_SEQ_EVENT), and writes
  *   d_counts [k][L] int32 (the reference's baseCounts columns, N only when k == 6),
  *   d_cov, d_pc (may be NULL), d_ent, d_sec  exactly as bc_stats defines them.
+ * Deep batches (many reads per tile) and spans > 4096 instead run the read-chunked kernel 1
+ * (each read decoded once, per-block LDS histograms, atomic flush into the zeroed counts)
+ * followed by kernel 2: three stream-ordered operations, same results.
  * Out-of-range counted events are recorded for bc_range_error() as with bc_count.
  * Overwrites its outputs; async; capturable.                                                   */
 int bc_pileup(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality, int k,

@@ -1,0 +1,103 @@
+"""Multi-process (one process per GPU) CLI paths on CPU: gloo, world_size 2.
+
+The counting itself needs a GPU; these tests cover what the ranks exchange: reference
+sharding, the per-reference gather to rank 0 and the ordered per-position output, checked to
+be byte-identical to a single process."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from basecount_amd.dist import shard
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "dist_worker.py")
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world: int, args, tmp_path, name, expect_fail=False, extra_env=None):
+    out = tmp_path / f"{name}.out"
+    env = dict(os.environ, **(extra_env or {}), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               WORLD_SIZE=str(world), BASECOUNT_DIST_BACKEND="gloo", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    with open(out, "ab") as fh:
+        procs = []
+        for r in range(world):
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+            if world == 1:
+                for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+                    e.pop(v)
+            procs.append(subprocess.Popen([sys.executable, WORKER, *args], stdout=fh,
+                                          stderr=subprocess.PIPE, env=e))
+        errs = [p.communicate(timeout=240)[1] for p in procs]
+    codes = [p.returncode for p in procs]
+    if expect_fail:  # rank 0 (which prints) raises; the launcher then fails the job
+        assert codes[0] != 0, codes
+        return out.read_bytes(), [e.decode().strip().splitlines()[-1] for e in errs]
+    assert codes == [0] * world, (codes, [e.decode()[-2000:] for e in errs])
+    return out.read_bytes()
+
+
+def test_shard_is_lpt_and_deterministic():
+    w = {"a": 10, "b": 9, "c": 5, "d": 5, "e": 1}
+    o = shard(list(w), w, 2)
+    assert o == shard(list(reversed(list(w))), w, 2)
+    loads = [sum(w[r] for r in w if o[r] == i) for i in range(2)]
+    assert sorted(loads) == [15, 15]
+    assert set(shard(list(w), w, 8).values()) <= set(range(8))
+
+
+@pytest.mark.parametrize("args", [["x.bam"], ["x.bam", "--long-format", "--show-n-bases"],
+                                  ["x.bam", "--summarise", "--decimal-places", "5"]])
+def test_cli_world2_matches_single_process(tmp_path, args):
+    single = _run(1, args, tmp_path, "single")
+    multi = _run(2, args, tmp_path, "multi")
+    assert len(single) > 500
+    assert multi == single
+
+
+def test_cli_world2_summary_with_bed(tmp_path):
+    bed = os.path.join(HERE, "golden", "scheme.bed")
+    args = ["x.bam", "--summarise-with-bed", bed]
+    assert _run(2, args, tmp_path, "multi") == _run(1, args, tmp_path, "single")
+
+
+def _gather_worker(path):
+    # run by subprocess: exercise Group.gather_bytes / all_gather_ints with ragged payloads
+    from basecount_amd.dist import Group
+
+    g = Group("gloo")
+    got = g.gather_bytes(b"r" * (3 + 1000 * g.rank))
+    ints = g.all_gather_ints([g.rank, 7])
+    if g.rank == 0:
+        with open(path, "w") as fh:
+            fh.write(repr(([len(x) for x in got], ints)))
+    g.close()
+
+
+def test_gather_bytes_ragged(tmp_path):
+    path = tmp_path / "g.txt"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2")
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import test_dist as t; "
+            "t._gather_worker(%r)" % (os.path.dirname(HERE), HERE, str(path)))
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
+             for r in range(2)]
+    assert [p.wait(timeout=240) for p in procs] == [0, 0]
+    assert path.read_text() == repr(([3, 1003], [[0, 7], [1, 7]]))
+
+
+def test_cli_world2_same_error_as_single_process(tmp_path):
+    """A zero-length reference makes the summary raise ZeroDivisionError (main.py:479); rank 0
+    raises it after the same output as a single process."""
+    env = {"FAKE_EMPTY_REF": "1"}
+    s_out, s_err = _run(1, ["x.bam", "--summarise"], tmp_path, "single", True, env)
+    m_out, m_err = _run(2, ["x.bam", "--summarise"], tmp_path, "multi", True, env)
+    assert s_err[0].startswith("ZeroDivisionError") and m_err[0] == s_err[0]
+    assert m_out == s_out

@@ -114,8 +114,21 @@ def main():
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU; BASECOUNT_DIST_BACKEND=gloo lets ranks share a GPU (rehearsals)
+        backend = os.environ.get("BASECOUNT_DIST_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        sys.stdout.flush()
+        saved = os.dup(1)  # the backends log connection messages on fd 1: rank 0 prints ONE line
+        try:
+            os.dup2(2, 1)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            else:
+                dist.init_process_group(backend)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
 
     from basecount_amd import device as D
     from basecount_amd import synth
@@ -129,7 +142,7 @@ def main():
     b = synth.batch_arrays(rs, 0, 0)
     L = rs.lengths[0]
     ncols = k = 5
-    ctx = D.Context(local if world > 1 else 0)  # library-owned non-blocking stream
+    ctx = D.Context(local % max(1, D.device_count()) if world > 1 else 0)  # own stream
     reads = D.DeviceReads(ctx, b)               # resident in HBM before anything is timed
     assert reads.r.sorted == 1
     counts = ctx.alloc(4 * ncols * L)
@@ -165,7 +178,7 @@ def main():
     elapsed = time.perf_counter() - t0
     dev_step = ctx.event_elapsed_ms(0, 1) * 1e-3 / args.steps  # s per step on the device
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -209,12 +222,15 @@ def main():
     # ---- gather per-contig coverage to rank 0 over RCCL (output step, outside the timing) ----
     gather_ms = None
     if dist:
-        covt = torch.from_numpy(dcov.download(np.int32, L)).cuda()
-        torch.cuda.synchronize()
+        covt = torch.from_numpy(dcov.download(np.int32, L))
+        if backend == "nccl":
+            covt = covt.cuda()
+            torch.cuda.synchronize()
         g0 = time.perf_counter()
-        bufs = [torch.zeros_like(covt) for _ in range(world)] if rank == 0 else None
-        dist.gather(covt, bufs, dst=0)
-        torch.cuda.synchronize()
+        bufs = [torch.zeros_like(covt) for _ in range(world)]
+        dist.all_gather(bufs, covt)  # per-contig coverage of every rank (RCCL over xGMI)
+        if backend == "nccl":
+            torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
 
     events = synth.ref_events(rs)

@@ -52,6 +52,7 @@ struct RcArgs {
     int64_t n_chunks;
     int32_t* counts;  // [ncols][L], accumulated into
     unsigned long long* err;
+    int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events
 };
 
 // Block-wide reduction of 8 values (max or min per slot): wave reduce, then LDS across waves.
@@ -79,7 +80,8 @@ __device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_
 // Fold a wave's window counters into the LDS histogram: 8-slot sums per lane group (DPP), then
 // each lane adds its own window position (s = lane & 7) for every column.
 template <int NC>
-__device__ __forceinline__ void rc_fold(Swar& W, uint32_t (*hist)[kRcWinPos], int g, int s8) {
+__device__ __forceinline__ void rc_fold(Swar& W, uint32_t (*hist)[kRcWinPos], int g, int s8, int ablate = 0) {
+    if (ablate & 128) return;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const uint32_t b0 = sum8(W.a4[c] & 0x0F0F0F0Fu), b1 = sum8((W.a4[c] >> 4) & 0x0F0F0F0Fu);
@@ -292,9 +294,10 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
             int g = 0, it4 = 0;
             while (g + 1 < nwin && U(wpre[g + 1]) <= k0) ++g;
             uint32_t gnext = U(wpre[g + 1]), gpre = U(wpre[g]), glo = U(wlo[g]), ghi = U(whi[g]);
-            for (uint32_t k = k0; k < k1; ++k) {
+            const uint32_t k1w = (A.ablate & 4) ? k0 : k1;
+            for (uint32_t k = k0; k < k1w; ++k) {
                 if (k >= gnext) {  // next window (wave-uniform)
-                    if (it4) rc_fold<NC>(W, hist, g, s8);
+                    if (it4) rc_fold<NC>(W, hist, g, s8, A.ablate);
                     it4 = 0;
                     while (k >= U(wpre[g + 1])) ++g;
                     gnext = U(wpre[g + 1]);
@@ -307,7 +310,9 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
                 const bool in = r < ghi;
                 const int rs = in ? (int)r : 0;
                 uint32_t x;
-                if (maxrun <= 1) {
+                if (A.ablate & 256) {
+                    x = rec[rs * 3].x * 0x01010101u;
+                } else if (maxrun <= 1) {
                     x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
                                       : window_events<1, true, false, QUAL>(src, rec, rs, gb))
                             : (staged ? window_events<1, false, true, QUAL>(src, rec, rs, gb)
@@ -329,11 +334,11 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
                 }
                 swar_add<NC>(W, x);
                 if (++it4 == 14) {
-                    rc_fold<NC>(W, hist, g, s8);
+                    rc_fold<NC>(W, hist, g, s8, A.ablate);
                     it4 = 0;
                 }
             }
-            if (it4) rc_fold<NC>(W, hist, g, s8);
+            if (it4) rc_fold<NC>(W, hist, g, s8, A.ablate);
             __syncthreads();
             // ---- 4. flush the pass's positions (< L) into the counts
             for (int t = tid; t < 8 * nwin; t += kRcThreads) {
@@ -395,6 +400,8 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     A.n_chunks = (r.n_reads + kRcReads - 1) / kRcReads;
     A.counts = counts;
     A.err = d_err;
+    A.ablate = 0;
+    if (const char* ab = std::getenv("BC_ABLATE")) A.ablate = std::atoi(ab);
     int64_t blocks = A.n_chunks < 256 * 4 ? A.n_chunks : 256 * 4;
     const dim3 grid((unsigned)blocks), block(kRcThreads);
     if (mbq > 0) {

@@ -57,6 +57,7 @@ struct PileArgs {
     unsigned long long* err;
     int64_t seq_words;   // readable 32-bit words of seq (bc_seq_event_bytes / 4)
     int64_t qual_bytes;
+    int64_t tiles_per_wave;  // k_pileup_solo: consecutive tiles swept by one wave
     int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 4 no walk, 8 no stats
                  // math, 16 no stores, 32 no sequence staging
 };
@@ -270,6 +271,132 @@ __host__ __device__ inline size_t pileup_lds_bytes(int nw, int groups) {
     return (size_t)nw * (kRecBytes + kStageRegion) + kFinBytes;
 }
 
+// One chunk of nr <= 64 reads [base, base + nr) of a tile, walked by one wave: load the reads'
+// fields, decode their CIGARs, stage their sequence into the wave's LDS region and walk them
+// (SWAR windows, or the per-position CIGAR walk for complex reads).  Counts accumulate in W /
+// cnt (lane = tile position t0 + lane), the first out-of-range read in `bad`.
+template <bool QUAL, int K>
+__device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, int nr, int lane, int s8, int gb,
+                                              int64_t t0, int64_t P, bool edge, bool beyond, uint32_t bmask,
+                                              uint4* myrec, uint8_t* mystage, bool qual_vec, Swar& W, int& it4,
+                                              uint32_t (&cnt)[6], unsigned long long& acc, int& pending,
+                                              int64_t& bad) {
+    // ---- chunk load: per-read fields lane-parallel, CIGAR -> run table (VALU)
+    RunTable T;
+    uint32_t mpos = 0, msn = 0, mcb = 0, mcn = 0;
+    T.nrun = 0;
+    T.complex = false;
+    T.gap = false;
+    T.span = 0;
+    T.qlen = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
+    if (lane < nr) {
+        const int64_t r = base + lane;
+        mpos = (uint32_t)A.pos[r];
+        mcb = A.cig_beg[r];
+        mcn = A.cig_n[r];
+        msn = A.seq_nib[r];
+    }
+    // ops to decode: the wave's largest CIGAR (more than kPre -> complex anyway)
+    const int cmax = (int)wave_reduce<true>(mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre);
+    if (lane < nr) {
+        uint32_t w[kPre];
+#pragma unroll
+        for (int i = 0; i < kPre; ++i) {
+            w[i] = 0u;
+            if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
+        }
+        T = decode_runs(w, mcn, cmax);
+    }
+    const bool cx = __any(T.complex);
+    const bool gap = __any(T.gap);
+    const int maxrun = (int)wave_reduce<true>((uint32_t)T.nrun);
+    // ---- stage the chunk's sequence (BC_SEQ_EVENT words) into LDS; with a quality
+    // threshold, bases below it are cleared here (count.cpp:56)
+    uint32_t blo = 0xFFFFFFFFu, bhi = 0;
+    if (lane < nr && T.qlen) {
+        blo = msn >> 1;
+        bhi = (msn + T.qlen + 1) >> 1;
+    }
+    uint32_t seg_lo = wave_reduce<false>(blo);
+    const uint32_t seg_hi = wave_reduce<true>(bhi);
+    seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
+    const bool staged = !cx && seg_hi - seg_lo <= (uint32_t)kStage && !(A.ablate & 32);
+    if (staged) {
+        for (uint32_t off = lane * 16u; off < seg_hi - seg_lo; off += 1024u) {
+            uint4 v = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
+            if (QUAL) {
+                const int64_t q0 = 2 * ((int64_t)seg_lo + off);  // first base of the piece
+                uint32_t qw[8];
+                if (qual_vec && q0 + 32 <= A.qual_bytes) {
+                    const uint4 qa = *(const uint4*)(A.qual + q0), qb = *(const uint4*)(A.qual + q0 + 16);
+                    qw[0] = qa.x, qw[1] = qa.y, qw[2] = qa.z, qw[3] = qa.w;
+                    qw[4] = qb.x, qw[5] = qb.y, qw[6] = qb.z, qw[7] = qb.w;
+                } else {
+                    for (int i = 0; i < 8; ++i) {
+                        qw[i] = 0;
+                        for (int bb = 0; bb < 4; ++bb) {
+                            const int64_t at = q0 + 4 * i + bb;
+                            if (at < A.qual_bytes) qw[i] |= (uint32_t)A.qual[at] << (8 * bb);
+                        }
+                    }
+                }
+                v.x &= qual_nibmask(qw[0], qw[1], A.mbq);
+                v.y &= qual_nibmask(qw[2], qw[3], A.mbq);
+                v.z &= qual_nibmask(qw[4], qw[5], A.mbq);
+                v.w &= qual_nibmask(qw[6], qw[7], A.mbq);
+            }
+            *(uint4*)(mystage + off) = v;
+        }
+    }
+    const uint32_t qbase = staged ? 2u * seg_lo : 0u;
+    if (cx) {  // walk_complex reads {pos, absolute seq_nib}
+        myrec[lane * 3] = make_uint4(mpos, msn, 0u, 0u);
+    } else {
+        uint32_t rr[kMaxRuns], nb[kMaxRuns];
+#pragma unroll
+        for (int k = 0; k < kMaxRuns; ++k) {
+            rr[k] = pack_rr(T.st[k], T.en[k]);
+            nb[k] = msn - qbase + (uint32_t)T.qd[k];
+        }
+        myrec[lane * 3] = make_uint4(mpos, T.span * 4u, rr[0], nb[0]);
+        myrec[lane * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
+        myrec[lane * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int64_t rbase = base;
+    if (A.ablate & 4) {
+    } else if (cx) {
+        if (pending + nr >= (1 << kField) - 1) {
+            flush_acc(acc, cnt);
+            pending = 0;
+        }
+        pending += nr;
+        walk_complex<QUAL>(A, myrec, nr, P, t0, rbase, edge && beyond, mcn, mcb, acc, bad);
+    } else {
+        // separate calls keep the LDS / global address spaces visible to the compiler
+#define BC_WALK(NR, GP, ST)                                                                                 \
+walk_swar<NR, GP, ST, QUAL, K>(A, myrec, ST ? (const uint32_t*)mystage : (const uint32_t*)A.seq, nr, gb,   \
+                       s8, rbase, edge, bmask, W, it4, cnt, bad)
+#define BC_WALK_NR(GP, ST)                                                                                  \
+do {                                                                                                    \
+if (maxrun <= 1) BC_WALK(1, GP, ST);                                                                \
+else if (maxrun == 2) BC_WALK(2, GP, ST);                                                           \
+else BC_WALK(4, GP, ST);                                                                            \
+} while (0)
+        if (staged) {
+            if (gap) BC_WALK_NR(true, true);
+            else BC_WALK_NR(false, true);
+        } else {
+            if (gap) BC_WALK_NR(true, false);
+            else BC_WALK_NR(false, false);
+        }
+#undef BC_WALK_NR
+#undef BC_WALK
+    }
+}
+
 template <bool QUAL, int K, bool STATS>
 __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
@@ -325,120 +452,8 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             uint8_t* mystage = stage_all + (size_t)wave * kStageRegion + 16;
             for (int64_t base = lo + (int64_t)ws * 64; base < hi; base += (int64_t)S * 64) {
                 const int nr = (int)((hi - base) < 64 ? (hi - base) : 64);
-                // ---- chunk load: per-read fields lane-parallel, CIGAR -> run table (VALU)
-                RunTable T;
-                uint32_t mpos = 0, msn = 0, mcb = 0, mcn = 0;
-                T.nrun = 0;
-                T.complex = false;
-                T.gap = false;
-                T.span = 0;
-                T.qlen = 0;
-#pragma unroll
-                for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
-                if (lane < nr) {
-                    const int64_t r = base + lane;
-                    mpos = (uint32_t)A.pos[r];
-                    mcb = A.cig_beg[r];
-                    mcn = A.cig_n[r];
-                    msn = A.seq_nib[r];
-                }
-                // ops to decode: the wave's largest CIGAR (more than kPre -> complex anyway)
-                const int cmax = (int)wave_reduce<true>(mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre);
-                if (lane < nr) {
-                    uint32_t w[kPre];
-#pragma unroll
-                    for (int i = 0; i < kPre; ++i) {
-                        w[i] = 0u;
-                        if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
-                    }
-                    T = decode_runs(w, mcn, cmax);
-                }
-                const bool cx = __any(T.complex);
-                const bool gap = __any(T.gap);
-                const int maxrun = (int)wave_reduce<true>((uint32_t)T.nrun);
-                // ---- stage the chunk's sequence (BC_SEQ_EVENT words) into LDS; with a quality
-                // threshold, bases below it are cleared here (count.cpp:56)
-                uint32_t blo = 0xFFFFFFFFu, bhi = 0;
-                if (lane < nr && T.qlen) {
-                    blo = msn >> 1;
-                    bhi = (msn + T.qlen + 1) >> 1;
-                }
-                uint32_t seg_lo = wave_reduce<false>(blo);
-                const uint32_t seg_hi = wave_reduce<true>(bhi);
-                seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
-                const bool staged = !cx && seg_hi - seg_lo <= (uint32_t)kStage && !(A.ablate & 32);
-                if (staged) {
-                    for (uint32_t off = lane * 16u; off < seg_hi - seg_lo; off += 1024u) {
-                        uint4 v = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
-                        if (QUAL) {
-                            const int64_t q0 = 2 * ((int64_t)seg_lo + off);  // first base of the piece
-                            uint32_t qw[8];
-                            if (qual_vec && q0 + 32 <= A.qual_bytes) {
-                                const uint4 qa = *(const uint4*)(A.qual + q0), qb = *(const uint4*)(A.qual + q0 + 16);
-                                qw[0] = qa.x, qw[1] = qa.y, qw[2] = qa.z, qw[3] = qa.w;
-                                qw[4] = qb.x, qw[5] = qb.y, qw[6] = qb.z, qw[7] = qb.w;
-                            } else {
-                                for (int i = 0; i < 8; ++i) {
-                                    qw[i] = 0;
-                                    for (int bb = 0; bb < 4; ++bb) {
-                                        const int64_t at = q0 + 4 * i + bb;
-                                        if (at < A.qual_bytes) qw[i] |= (uint32_t)A.qual[at] << (8 * bb);
-                                    }
-                                }
-                            }
-                            v.x &= qual_nibmask(qw[0], qw[1], A.mbq);
-                            v.y &= qual_nibmask(qw[2], qw[3], A.mbq);
-                            v.z &= qual_nibmask(qw[4], qw[5], A.mbq);
-                            v.w &= qual_nibmask(qw[6], qw[7], A.mbq);
-                        }
-                        *(uint4*)(mystage + off) = v;
-                    }
-                }
-                const uint32_t qbase = staged ? 2u * seg_lo : 0u;
-                if (cx) {  // walk_complex reads {pos, absolute seq_nib}
-                    myrec[lane * 3] = make_uint4(mpos, msn, 0u, 0u);
-                } else {
-                    uint32_t rr[kMaxRuns], nb[kMaxRuns];
-#pragma unroll
-                    for (int k = 0; k < kMaxRuns; ++k) {
-                        rr[k] = pack_rr(T.st[k], T.en[k]);
-                        nb[k] = msn - qbase + (uint32_t)T.qd[k];
-                    }
-                    myrec[lane * 3] = make_uint4(mpos, T.span * 4u, rr[0], nb[0]);
-                    myrec[lane * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
-                    myrec[lane * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
-                }
-                __builtin_amdgcn_wave_barrier();
-                const int64_t rbase = base;
-                if (A.ablate & 4) {
-                } else if (cx) {
-                    if (pending + nr >= (1 << kField) - 1) {
-                        flush_acc(acc, cnt);
-                        pending = 0;
-                    }
-                    pending += nr;
-                    walk_complex<QUAL>(A, myrec, nr, P, t0, rbase, edge && beyond, mcn, mcb, acc, bad);
-                } else {
-                    // separate calls keep the LDS / global address spaces visible to the compiler
-#define BC_WALK(NR, GP, ST)                                                                                 \
-    walk_swar<NR, GP, ST, QUAL, K>(A, myrec, ST ? (const uint32_t*)mystage : (const uint32_t*)A.seq, nr, gb,   \
-                                   s8, rbase, edge, bmask, W, it4, cnt, bad)
-#define BC_WALK_NR(GP, ST)                                                                                  \
-    do {                                                                                                    \
-        if (maxrun <= 1) BC_WALK(1, GP, ST);                                                                \
-        else if (maxrun == 2) BC_WALK(2, GP, ST);                                                           \
-        else BC_WALK(4, GP, ST);                                                                            \
-    } while (0)
-                    if (staged) {
-                        if (gap) BC_WALK_NR(true, true);
-                        else BC_WALK_NR(false, true);
-                    } else {
-                        if (gap) BC_WALK_NR(true, false);
-                        else BC_WALK_NR(false, false);
-                    }
-#undef BC_WALK_NR
-#undef BC_WALK
-                }
+                process_chunk<QUAL, K>(A, base, nr, lane, s8, gb, t0, P, edge, beyond, bmask, myrec, mystage,
+                                       qual_vec, W, it4, cnt, acc, pending, bad);
                 __builtin_amdgcn_wave_barrier();
             }
             flush_acc(acc, cnt);
@@ -515,6 +530,148 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     }
 }
 
+// ---- sparse batches (at most ~48 reads per tile): one wave per tile, tiles swept in order ----
+
+// Kernel 2 for one position from its counts (main.py:29-53 in CPython's order, the same
+// arithmetic as tile_terms + the ordered sums of k_pileup), written by the position's lane.
+template <int K>
+__device__ __forceinline__ void pos_stats(const PileArgs& A, const uint32_t* c, int64_t P) {
+    const int64_t L = A.L;
+    int64_t cov = 0;
+    int am = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        cov += c[j];
+        if (c[j] > c[am]) am = j;  // np.argmax: first maximum
+    }
+    A.cov[P] = (int32_t)cov;
+    double h = 1.0, h2 = 1.0;
+    if (cov != 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const double pj = (double)c[j] / (double)cov;
+            if (A.pc) A.pc[(int64_t)j * L + P] = 100.0 * pj;
+            if (c[j] != 0) s = s + (-(pj * log2(pj)));
+        }
+        h = A.nf * s;
+        const int64_t cov2 = cov - c[am];
+        if (cov2 != 0) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (j != am && c[j] != 0) {
+                    const double q = (double)c[j] / (double)cov2;
+                    s2 = s2 + (-(q * log2(q)));
+                }
+            h2 = A.nf2 * s2;
+        }
+    } else if (A.pc) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) A.pc[(int64_t)j * L + P] = -1.0;
+    }
+    A.ent[P] = h;
+    A.sec[P] = h2;
+}
+
+// Move a read cursor forward to the first index >= cur whose pos >= key (pos is sorted and the
+// keys of successive tiles increase).  `win` holds pos[wbase + lane]: the 64 reads after the
+// cursor are looked at with one ballot, refilled only when the cursor leaves them.
+__device__ __forceinline__ void advance_cursor(const int32_t* pos, int64_t n, int64_t& cur, int64_t key, int32_t& win,
+                                               int64_t& wbase, int lane) {
+    for (;;) {
+        if (cur >= n) return;
+        if (cur >= wbase + 64) {
+            wbase = cur;
+            const int64_t i = wbase + lane;
+            win = i < n ? pos[i] : INT32_MAX;
+        }
+        const int below = __popcll(__ballot((int64_t)win < key));  // a prefix of the window
+        int64_t end = wbase + below;
+        end = end < n ? end : n;
+        if (end > cur) cur = end;
+        if (below < 64 || cur >= n) return;
+        cur = wbase + 64;
+    }
+}
+
+// Sparse batches: every wave owns a contiguous run of tiles and sweeps it with two read cursors
+// (no per-tile search), walks the few reads of each tile alone, and computes the statistics of
+// its own positions in registers: no block barriers at all.  Empty tiles only store.
+template <bool QUAL, int K, bool STATS>
+__global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = blockDim.x >> 6;
+    uint4* myrec = (uint4*)dyn + wave * kTile * 3;
+    uint8_t* mystage = dyn + (size_t)nw * kRecBytes + (size_t)wave * kStageRegion + 16;
+    const int64_t L = A.L;
+    const int s8 = lane & 7;
+    const bool qual_vec = ((uintptr_t)A.qual & 15u) == 0;
+    const int64_t G = gridDim.x;
+    const int64_t lb = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
+    const int64_t t_begin = (lb * nw + wave) * A.tiles_per_wave;
+    const int64_t t_end = t_begin + A.tiles_per_wave < A.n_tiles ? t_begin + A.tiles_per_wave : A.n_tiles;
+    if (t_begin >= t_end) return;  // no barriers in this kernel
+    int64_t lo, hi;
+    lower_bound_pair(A.pos, A.n, t_begin * kTile - A.max_span + 1, t_begin * kTile + kTile, lane, lo, hi);
+    int64_t wlo_base = lo, whi_base = hi;
+    int32_t wlo = lo + lane < A.n ? A.pos[lo + lane] : INT32_MAX;
+    int32_t whi = hi + lane < A.n ? A.pos[hi + lane] : INT32_MAX;
+    for (int64_t t = t_begin; t < t_end; ++t) {
+        const int64_t t0 = t * kTile;
+        const int64_t P = t0 + lane;
+        const int gb = (int)t0 + 8 * (lane >> 3);
+        if (t > t_begin) {
+            advance_cursor(A.pos, A.n, lo, t0 - A.max_span + 1, wlo, wlo_base, lane);
+            advance_cursor(A.pos, A.n, hi, t0 + kTile, whi, whi_base, lane);
+        }
+        uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
+        if (hi > lo) {
+            int64_t bad = INT64_MAX;
+            const bool edge = t0 + kTile > L;
+            const bool beyond = P >= L;
+            uint32_t bmask = 0;
+            if (edge) {
+                int64_t kL = L - gb;
+                kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
+                bmask = ~(lo32_bit(4 * (int)kL) - 1u);
+            }
+            unsigned long long acc = 0;
+            int pending = 0;
+            Swar W;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) W.a4[c] = 0;
+            int it4 = 0;
+            for (int64_t base = lo; base < hi; base += 64) {
+                const int nr = (int)((hi - base) < 64 ? (hi - base) : 64);
+                process_chunk<QUAL, K>(A, base, nr, lane, s8, gb, t0, P, edge, beyond, bmask, myrec, mystage,
+                                       qual_vec, W, it4, cnt, acc, pending, bad);
+                __builtin_amdgcn_wave_barrier();
+            }
+            flush_acc(acc, cnt);
+            if (it4) swar_fold<K>(W, cnt, s8);
+            if (edge) {
+                for (int o = 32; o > 0; o >>= 1) {
+                    const int64_t b2 = __shfl_down(bad, o);
+                    bad = b2 < bad ? b2 : bad;
+                }
+                if (lane == 0 && bad != INT64_MAX) atomicMin(A.err, (unsigned long long)bad);
+            }
+        }
+        if (t0 < L && P < L && !(A.ablate & 16)) {
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                int32_t* dst = A.counts + (int64_t)c * L + P;
+                if (A.accumulate) cnt[c] += (uint32_t)*dst;
+                *dst = (int32_t)cnt[c];
+            }
+            if (STATS) pos_stats<K>(A, cnt, P);
+        }
+    }
+}
+
 PileArgs make_args(const bc_reads& r, int64_t L, uint32_t mbq) {
     PileArgs A;
     std::memset(&A, 0, sizeof A);
@@ -560,6 +717,34 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
     while (S < 8 && per_tile > 48.0 * S) S *= 2;
     if (const char* e = std::getenv("BC_TILE_WAVES")) S = std::max(1, std::min(8, std::atoi(e)));
     A.S = S;
+    if (S == 1 && !std::getenv("BC_NO_SOLO")) {
+        // sparse: waves sweep contiguous tile runs; ~2 rounds of resident waves (256 CUs x 16)
+        const int nw = 4;
+        const int64_t target_waves = 256 * 16 * 2;
+        A.tiles_per_wave = (A.n_tiles + target_waves - 1) / target_waves;
+        if (A.tiles_per_wave < 1) A.tiles_per_wave = 1;
+        const int64_t waves = (A.n_tiles + A.tiles_per_wave - 1) / A.tiles_per_wave;
+        int64_t blocks = (waves + nw - 1) / nw;
+        blocks = (blocks + 7) / 8 * 8;  // a multiple of the XCD count (see the kernel's tile mapping)
+        const dim3 grid((unsigned)blocks), block(64 * nw);
+        const size_t lds = (size_t)nw * (kRecBytes + kStageRegion);
+#define BC_SOLO(Q, KK, ST) hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST>), grid, block, lds, s, A)
+        if (mbq > 0) {
+            if (k == 5) {
+                if (stats) BC_SOLO(true, 5, true); else BC_SOLO(true, 5, false);
+            } else {
+                if (stats) BC_SOLO(true, 6, true); else BC_SOLO(true, 6, false);
+            }
+        } else {
+            if (k == 5) {
+                if (stats) BC_SOLO(false, 5, true); else BC_SOLO(false, 5, false);
+            } else {
+                if (stats) BC_SOLO(false, 6, true); else BC_SOLO(false, 6, false);
+            }
+        }
+#undef BC_SOLO
+        return hipGetLastError();
+    }
     const int nw = S >= 4 ? S : 4;
     const int groups = nw / S;
     int64_t blocks = (A.n_tiles + groups - 1) / groups;

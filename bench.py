@@ -8,6 +8,9 @@ scaling, no collective inside the step); the per-contig results are gathered to 
 RCCL once after the timed region (reported as gather_ms).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+
+C5 (24 human-chromosome-sized contigs, 3.09 Gb, 1.2 M reads) is summary-shaped: the per-position
+percentages are not stored (main.py's --summarise never prints them).
 """
 from __future__ import annotations
 
@@ -29,6 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 WORKLOADS = {
     "c2": "C2: 1 contig 29,903 bp, 100,000 reads x 150 bp, all-M CIGAR (per rank)",
     "c3": "C3: 1 contig 29,903 bp, 1,000,000 reads x 150 bp, mixed M/I/D/=/X/S CIGAR (per rank)",
+    "c5": "C5: 24 contigs with GRCh38 chr1-22,X,Y lengths (3.09 Gb), 50,000 reads x 150 bp each, "
+          "all-M CIGAR; contigs sharded over the ranks",
 }
 
 
@@ -134,25 +139,45 @@ def main():
     from basecount_amd import synth
     from basecount_amd.main import norm_factors
 
-    # ---- workload: this rank's contig (weak scaling: one contig per rank) --------------------
-    name = "MN908947.3" if world == 1 else f"contig{rank}"
+    # ---- workload: this rank's contigs -----------------------------------------------------
+    # c2 / c3: one contig of the config's shape per rank (weak scaling); c5: the 24 GRCh38-sized
+    # contigs, sharded over the ranks by LPT (strong scaling: the total work is fixed)
     c = synth.CONFIGS[args.config]
-    rs = synth.make_reads([(name, c["contigs"][0][1])], c["reads"], c["mixed"],
-                          c["seed"] + 1000 * rank)
-    b = synth.batch_arrays(rs, 0, 0)
-    L = rs.lengths[0]
+    per_contig = c.get("per_contig", False)
+    if per_contig:
+        from basecount_amd.dist import shard
+
+        contigs = list(c["contigs"])
+        owner = shard([n for n, _ in contigs], dict(contigs), world)
+        mine = [(n, L) for n, L in contigs if owner[n] == rank]
+        rs = synth.make_reads(mine, c["reads"], c["mixed"], c["seed"] + 1000 * rank)
+        total_positions = sum(L for _, L in contigs)
+    else:
+        name = "MN908947.3" if world == 1 else f"contig{rank}"
+        rs = synth.make_reads([(name, c["contigs"][0][1])], c["reads"], c["mixed"],
+                              c["seed"] + 1000 * rank)
+        total_positions = world * rs.lengths[0]
     ncols = k = 5
+    want_pc = not per_contig  # c5 is only ever summarised: no per-position percentages
     ctx = D.Context(local % max(1, D.device_count()) if world > 1 else 0)  # own stream
-    reads = D.DeviceReads(ctx, b)               # resident in HBM before anything is timed
-    assert reads.r.sorted == 1
-    counts = ctx.alloc(4 * ncols * L)
-    dcov, dpc, dent, dsec = ctx.alloc(4 * L), ctx.alloc(8 * k * L), ctx.alloc(8 * L), ctx.alloc(8 * L)
     nf, nf2 = norm_factors(k)
+    work = []  # one entry per contig, resident in HBM before anything is timed
+    for t, L in enumerate(rs.lengths):
+        b = synth.batch_arrays(rs, t, 0)
+        reads = D.DeviceReads(ctx, b)
+        assert reads.r.sorted == 1
+        bufs = dict(counts=ctx.alloc(4 * ncols * L), cov=ctx.alloc(4 * L),
+                    pc=ctx.alloc(8 * k * L) if want_pc else None, ent=ctx.alloc(8 * L), sec=ctx.alloc(8 * L))
+        work.append((t, L, b, reads, bufs))
+
+    def ptr(x):
+        return x.ptr if x is not None else None
 
     def step():
-        # one pass of the hot path: fused CIGAR-expand/count + statistics, one launch
-        ctx.pileup(reads, L, args.mbq, k, nf, nf2, counts.ptr, dcov.ptr, dpc.ptr, dent.ptr,
-                   dsec.ptr)
+        # one pass of the hot path over every contig of this rank: kernel 1 + kernel 2
+        for _, L, _, reads, o in work:
+            ctx.pileup(reads, L, args.mbq, k, nf, nf2, o["counts"].ptr, o["cov"].ptr, ptr(o["pc"]),
+                       o["ent"].ptr, o["sec"].ptr)
 
     for _ in range(args.warmup):
         step()
@@ -185,7 +210,7 @@ def main():
     # ---- which kernels a step launches (library timing facility, per-launch event pairs) -------
     ctx.timing(True)
     step()
-    launched = [name for name in ctx.timing_report()]
+    launched = sorted(ctx.timing_report())
     ctx.timing(False)
 
     def region(fn, reps):  # on-device seconds per call: hipEvents around `reps` back-to-back calls
@@ -196,33 +221,53 @@ def main():
         ctx.event_record(3)
         return ctx.event_elapsed_ms(2, 3) * 1e-3 / reps
 
-    # per-kernel average durations, each timed as a region of back-to-back launches of that
-    # kernel alone (a one-kernel step: the step region itself)
+    # per-kernel time per step, each timed as a region of back-to-back launches of that kernel
+    # alone (a one-kernel step: the step region itself)
     kern_s = {}
     if launched == ["pileup"]:
         kern_s["pileup"] = dev_step
-    else:  # deep batch: memset + k_rc + k_stats (bc_count on the same batch launches k_rc alone)
-        reps = max(5, min(args.steps, 50))
-        kern_s["rc"] = region(lambda: ctx.count(reads, L, args.mbq, k, counts.ptr), reps)
-        kern_s["stats"] = region(lambda: ctx.stats(counts.ptr, L, k, nf, nf2, dcov.ptr, dpc.ptr, dent.ptr,
-                                                   dsec.ptr), reps)
-        step()  # restore the step's outputs (the count-only regions accumulated into `counts`)
+    else:  # deep batches: memset + k_rc + k_stats (bc_count on the same batch launches k_rc alone)
+        reps = max(3, min(args.steps, 50))
+
+        def count_only():
+            for _, L, _, reads, o in work:
+                ctx.count(reads, L, args.mbq, k, o["counts"].ptr)
+
+        def stats_only():
+            for _, L, _, _, o in work:
+                ctx.stats(o["counts"].ptr, L, k, nf, nf2, o["cov"].ptr, ptr(o["pc"]), o["ent"].ptr,
+                          o["sec"].ptr)
+
+        kern_s["rc"] = region(count_only, reps)
+        kern_s["stats"] = region(stats_only, reps)
+        step()  # restore the step's outputs (the count-only regions accumulated into the counts)
         ctx.sync()
     dom = max(kern_s, key=kern_s.get)
 
-    # ---- correctness of what was timed (rank-local): counts vs the oracle -------------------
-    got = counts.download(np.int32, ncols * L).reshape(ncols, L)
+    # ---- correctness of what was timed (rank-local) -----------------------------------------
     import oracle as O
 
-    exp, _ = O.bcount(L, args.mbq, b)
-    parity = bool(np.array_equal(got, exp[:, :ncols].T.astype(np.int32)))
-    _, _, oent, _ = O.stats(exp, False)
-    parity = parity and float(np.max(np.abs(dent.download(np.float64, L) - oent))) <= 1e-6
+    parity = True
+    small = min(work, key=lambda w: w[1])  # full oracle check on the smallest contig
+    for t, L, b, reads, o in work:
+        if (t, L) == small[:2]:
+            got = o["counts"].download(np.int32, ncols * L).reshape(ncols, L)
+            exp, _ = O.bcount(L, args.mbq, b)
+            parity = parity and bool(np.array_equal(got, exp[:, :ncols].T.astype(np.int32)))
+            _, _, oent, _ = O.stats(exp, False)
+            parity = parity and float(np.max(np.abs(o["ent"].download(np.float64, L) - oent))) <= 1e-6
+            del got, exp, oent
+        if args.mbq == 0 and not c["mixed"]:
+            # size-independent check on every contig: all-M reads without N bases put every
+            # reference-consuming event into the coverage (a checksum of checksums)
+            cov_sum = int(o["cov"].download(np.int32, L).astype(np.int64).sum())
+            parity = parity and cov_sum == synth.ref_events(rs, t)
 
     # ---- gather per-contig coverage to rank 0 over RCCL (output step, outside the timing) ----
     gather_ms = None
-    if dist:
-        covt = torch.from_numpy(dcov.download(np.int32, L))
+    if dist and not per_contig:
+        L0, o0 = work[0][1], work[0][4]
+        covt = torch.from_numpy(o0["cov"].download(np.int32, L0))
         if backend == "nccl":
             covt = covt.cuda()
             torch.cuda.synchronize()
@@ -235,9 +280,9 @@ def main():
 
     events = synth.ref_events(rs)
     ms = elapsed / args.steps * 1e3
-    positions = world * L * args.steps
-    rb = read_bytes(b, args.mbq, rs.l_seq)
-    kbytes = kernel_bytes(dom, rb, L, k)
+    positions = total_positions * args.steps
+    kbytes = sum(kernel_bytes(dom, read_bytes(b, args.mbq, rs.l_seq[rs.tid == t]), L, k, want_pc)
+                 for t, L, b, _, _ in work)
     achieved = kbytes / kern_s[dom] / 1e9
     kernel_names = {"pileup": "k_pileup (fused kernel 1 + 2)", "rc": "k_rc (read-chunked kernel 1)",
                     "stats": "k_stats (kernel 2)"}
@@ -246,13 +291,15 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as fh:
             pm = json.load(fh).get(args.config, {})
-        if pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom:
+        if pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom and world == 1:
             traffic = pm.get("hbm_bytes_per_launch")
+    n_reads = sum(int(w[2]["pos"].size) for w in work)
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(rs, b, L, args.cpu_budget)
+        if world == 1 and not args.no_cpu_baseline and not per_contig:
+            b0, L0 = work[0][2], work[0][1]
+            cpu = cpu_baseline(rs, b0, L0, args.cpu_budget)
         value = positions / elapsed
         line = {
             "metric": "reference positions/sec (kernel 1 + kernel 2, inputs resident in HBM)",
@@ -263,18 +310,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if per_contig else "weak",
             "vs_baseline": None,
             "dtype": "int32 counts / f64 stats",
             "data": "synthetic (seeded, BASELINE config shape)",
-            "config": {"workload": WORKLOADS[args.config], "reads_per_rank": int(b["pos"].size),
-                       "positions_per_rank": L, "min_base_quality": args.mbq,
+            "config": {"workload": WORKLOADS[args.config], "reads_per_rank": n_reads,
+                       "positions_per_rank": int(sum(w[1] for w in work)), "contigs_per_rank": len(work),
+                       "min_base_quality": args.mbq, "percentages_stored": want_pc,
                        "parallelism": f"contig-sharded x{world}"},
-            "gbases_piled_per_s": world * events * args.steps / elapsed / 1e9,
+            "gbases_piled_per_s": (world if not per_contig else 1) * events * args.steps / elapsed / 1e9,
             "device_us_per_step": dev_step * 1e6,
             "kernel_us": {kernel_names[n]: v * 1e6 for n, v in kern_s.items()},
-            "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per step" if dom == "pileup"
-                        else "memset + k_rc (kernel 1) + k_stats (kernel 2) per step") + ", eager launches",
+            "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per contig per step"
+                        if dom == "pileup" else "memset + k_rc (kernel 1) + k_stats (kernel 2) per contig per step")
+                       + ", eager launches",
             "parity_vs_oracle": parity,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

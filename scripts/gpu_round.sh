@@ -22,6 +22,8 @@ for s in $STEPS; do
     bench3) run bench3 600 python bench.py --config c3 --no-cpu-baseline ${BENCH_ARGS} ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --steps 200 ${BENCH_ARGS} ;;
+    prof5) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+           run prof5 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5 -o run -- python bench.py --no-cpu-baseline --steps 5 --warmup 1 --config c5 ${BENCH_ARGS} ;;
     prof3) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
            run prof3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- python bench.py --no-cpu-baseline --steps 200 --config c3 ${BENCH_ARGS} ;;
   esac

@@ -30,6 +30,7 @@ namespace {
 constexpr int kRcThreads = 256;
 constexpr int kRcReads = 256;   // reads per chunk (one per thread at setup)
 constexpr int kStage = 19968;   // staged sequence bytes per chunk (256 reads x 150 bp fit)
+constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's first base
 #include "bc_walk.h"
 
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
@@ -52,7 +53,8 @@ struct RcArgs {
     int64_t n_chunks;
     int32_t* counts;  // [ncols][L], accumulated into
     unsigned long long* err;
-    int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events
+    int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events,
+                 // 512 no staging, 2048 no flush
 };
 
 // Block-wide reduction of 8 values (max or min per slot): wave reduce, then LDS across waves.
@@ -147,6 +149,23 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
     auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     int64_t bad = INT64_MAX;
 
+    // the next chunk's per-read fields are loaded while the current one is walked
+    uint32_t fpos = 0x7FFFFFFFu, fsn = 0, fcb = 0, fcn = 0, fsn_first = 0, fsn_last = 0;
+    auto fetch_fields = [&](int64_t ch) {
+        if (ch >= A.n_chunks) return;
+        const int64_t b0 = ch * kRcReads;
+        const int n = (int)(A.n - b0 < kRcReads ? A.n - b0 : kRcReads);
+        if (tid < n) {
+            fpos = (uint32_t)A.pos[b0 + tid];
+            fcb = A.cig_beg[b0 + tid];
+            fcn = A.cig_n[b0 + tid];
+            fsn = A.seq_nib[b0 + tid];
+        }
+        fsn_first = A.seq_nib[b0];  // speculative staging bounds (reads usually lie in file order)
+        fsn_last = A.seq_nib[b0 + n - 1];
+    };
+    fetch_fields(blockIdx.x);
+
     for (int64_t chunk = blockIdx.x; chunk < A.n_chunks; chunk += gridDim.x) {
         const int64_t c0 = chunk * kRcReads;
         const int nr = (int)(A.n - c0 < kRcReads ? A.n - c0 : kRcReads);
@@ -154,11 +173,22 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
         const bool valid = tid < nr;
         uint32_t mpos = 0x7FFFFFFFu, msn = 0, mcb = 0, mcn = 0;
         if (valid) {
-            mpos = (uint32_t)A.pos[c0 + tid];
-            mcb = A.cig_beg[c0 + tid];
-            mcn = A.cig_n[c0 + tid];
-            msn = A.seq_nib[c0 + tid];
+            mpos = fpos;
+            mcb = fcb;
+            mcn = fcn;
+            msn = fsn;
         }
+        // speculative staging: the chunk's sequence usually lies in [first read's seq_nib, last
+        // read's seq_nib + one read): staged now, in parallel with the CIGAR loads, and checked
+        // against the exact bounds after the decode
+        uint32_t spec_lo = (U(fsn_first) >> 1) & ~15u;
+        uint32_t spec_hi = (U(fsn_last) >> 1) + kSpecSlack;
+        const uint32_t buf_end = (uint32_t)(A.seq_words * 4 < 0xFFFFFFFFll ? A.seq_words * 4 : 0xFFFFFFFFll);
+        spec_hi = spec_hi < buf_end ? spec_hi : buf_end;
+        const bool spec = !QUAL && spec_hi > spec_lo && spec_hi - spec_lo <= (uint32_t)kStage && !(A.ablate & 512);
+        if (spec)
+            for (uint32_t off = tid * 16u; off < spec_hi - spec_lo; off += kRcThreads * 16u)
+                *(uint4*)(stage + off) = *(const uint4*)(A.seq + spec_lo + off);
         RunTable T;
         T.nrun = 0;
         T.gap = T.complex = false;
@@ -204,10 +234,13 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
         const int maxspan = (int)v[4], maxrun = (int)v[5];
         const bool gap = v[6] != 0;
         seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
-        const bool staged = seg_hi - seg_lo <= (uint32_t)kStage;
         if (cx) cxl[atomicAdd(&ncx, 1u)] = (uint32_t)tid;
-        // ---- stage the chunk's sequence (16 B per thread per pass)
-        if (staged) {
+        const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
+        if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
+        const bool staged = spec_ok || seg_hi - seg_lo <= (uint32_t)kStage;
+        if (spec && !spec_ok) __syncthreads();  // (uniform) the speculative copy is overwritten
+        // ---- stage the chunk's sequence exactly (16 B per thread per pass) unless done above
+        if (staged && !spec_ok && !(A.ablate & 512)) {
             for (uint32_t off = tid * 16u; off < seg_hi - seg_lo; off += kRcThreads * 16u) {
                 uint4 q4 = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
                 if (QUAL) {
@@ -248,6 +281,7 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
             rec[tid * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
         }
         __syncthreads();  // stage, records and the complex-read list complete
+        fetch_fields(chunk + gridDim.x);  // in flight during the walk
         const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
                          staged ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
         const int64_t WB = P0 & ~(int64_t)7;
@@ -257,19 +291,36 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
             const int nwin = (int)(NW - wp < kRcWin ? NW - wp : kRcWin);
             const int64_t PB = WB + 8 * wp;
             for (int t = tid; t < 3 * kRcWinPos; t += kRcThreads) (&hist[0][0])[t] = 0u;
+            // reads overlapping window g are those with pos in [gb - maxspan + 1, gb + 8); pos is
+            // sorted, so both ends are monotone in g: read t is the boundary for the windows
+            // between its window and the next read's (no search, every entry written once)
+            if (tid < nr) {
+                auto win_of = [&](int64_t p) {  // window index of position p, clipped to [0, nwin]
+                    const int64_t w = p >= PB ? (p - PB) >> 3 : -1;
+                    return (int)(w < 0 ? 0 : (w > nwin ? nwin : w));
+                };
+                const int64_t p_t = rec[tid * 3].x;
+                const int64_t p_n = tid + 1 < nr ? (int64_t)rec[(tid + 1) * 3].x : INT64_MAX / 2;
+                // hi: b_g = #{pos < gb + 8} = t + 1 for g in [win(p_t), win(p_next))
+                const int b0 = tid == 0 ? 0 : win_of(p_t), b1 = tid + 1 < nr ? win_of(p_n) : nwin;
+                if (tid == 0)
+                    for (int g2 = 0; g2 < win_of(p_t); ++g2) whi[g2] = 0;
+                for (int g2 = (tid == 0 ? win_of(p_t) : b0); g2 < b1; ++g2) whi[g2] = (uint32_t)tid + 1;
+                // lo: a_g = #{pos + maxspan - 1 < gb} = t + 1 for g in [win(u_t) + 1, win(u_next) + 1)
+                const int64_t u_t = p_t + maxspan - 1, u_n = p_n + maxspan - 1;
+                const int a0 = win_of(u_t) + (u_t >= PB ? 1 : 0);
+                const int a1 = tid + 1 < nr ? win_of(u_n) + (u_n >= PB ? 1 : 0) : nwin;
+                if (tid == 0)
+                    for (int g2 = 0; g2 < (a0 < nwin ? a0 : nwin); ++g2) wlo[g2] = 0;
+                for (int g2 = a0; g2 < (a1 < nwin ? a1 : nwin); ++g2) wlo[g2] = (uint32_t)tid + 1;
+            } else if (nr == 0 && tid < nwin) {
+                wlo[tid] = whi[tid] = 0;
+            }
+            __syncthreads();  // window read ranges complete
             if (wave == 0) {
-                // reads overlapping window t: pos in [gb - maxspan + 1, gb + 8) (sorted records)
                 uint32_t cnt = 0;
                 if (lane < nwin) {
-                    const int64_t gb = PB + 8 * lane;
-                    const int64_t lo_key = gb - maxspan + 1, hi_key = gb + 8;
-                    uint32_t a = 0, b = 0;
-                    for (uint32_t step = kRcReads; step; step >>= 1) {  // branch-free lower bounds
-                        if (a + step <= (uint32_t)nr && (int64_t)rec[(a + step - 1) * 3].x < lo_key) a += step;
-                        if (b + step <= (uint32_t)nr && (int64_t)rec[(b + step - 1) * 3].x < hi_key) b += step;
-                    }
-                    wlo[lane] = a;
-                    whi[lane] = b;
+                    const uint32_t a = wlo[lane], b = whi[lane];
                     cnt = b > a ? (b - a + 63) / 64 : 0u;
                 }
                 // exclusive prefix of the item counts over the windows (DPP scan)
@@ -341,7 +392,7 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
             if (it4) rc_fold<NC>(W, hist, g, s8, A.ablate);
             __syncthreads();
             // ---- 4. flush the pass's positions (< L) into the counts
-            for (int t = tid; t < 8 * nwin; t += kRcThreads) {
+            for (int t = tid; t < ((A.ablate & 2048) ? 0 : 8 * nwin); t += kRcThreads) {
                 const int64_t p = PB + t;
                 if (p >= A.L) break;
 #pragma unroll

@@ -120,6 +120,8 @@ def make_reads(contigs, reads_per_contig: int, mixed: bool, seed: int, read_len:
     codes = ACGT[rng.integers(0, 4, (n, read_len))]
     if mixed and n_frac > 0:
         codes[rng.random((n, read_len)) < n_frac] = CODE_N
+    if read_len % 2:  # odd length: the last byte's low nibble is padding (0)
+        codes = np.pad(codes, ((0, 0), (0, 1)))
     packed = ((codes[:, 0::2] << 4) | codes[:, 1::2]).astype(np.uint8)
     qual = rng.integers(2, 41, (n, read_len)).astype(np.uint8)
     nb = (read_len + 1) // 2

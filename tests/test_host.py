@@ -154,3 +154,31 @@ def test_synth_event_checksum():
     ops, lens = cig & 15, cig >> 4
     assert synth.ref_events(rs) == int(lens[np.isin(ops, [0, 2, 3, 7, 8])].sum())
     assert math.isclose(synth.ref_events(rs) / 300, 150, rel_tol=0.1)
+
+
+@pytest.mark.parametrize("inflater", ["libdeflate", "zlib"])
+def test_bam_odd_length_quals(tmp_path, monkeypatch, inflater):
+    """QUAL lands at nibble index 2*seq_off + i with the pad byte of an odd-length read = 0xFF
+    (the decoder leaves no byte of its output arrays unwritten); both inflaters agree."""
+    if inflater == "zlib":
+        monkeypatch.setenv("BCIO_ZLIB", "1")
+    rs = synth.make_reads([("chrA", 2_000), ("chrB", 900)], 300, True, 23, read_len=151)
+    path = str(tmp_path / "odd.bam")
+    synth.write_bam(rs, path)
+    with BamFile(path) as f:
+        assert np.array_equal(f.seq, rs.seq)
+        assert np.array_equal(f.qual, synth._nibble_qual(rs))
+        assert np.array_equal(f.l_seq, rs.l_seq)
+
+
+def test_bam_corrupt_block(tmp_path):
+    """A damaged deflate stream is an error, not a silently short read set."""
+    rs = synth.make_reads([("chrA", 2_000)], 200, False, 5)
+    path = str(tmp_path / "bad.bam")
+    synth.write_bam(rs, path)
+    data = bytearray(open(path, "rb").read())
+    mid = len(data) // 2
+    data[mid: mid + 64] = bytes(64)
+    open(path, "wb").write(bytes(data))
+    with pytest.raises(Exception):
+        BamFile(path)

@@ -770,8 +770,22 @@ int py_repr(double y, char* out) {
     return (int)(o - out);
 }
 
+// Fast path for dp <= 4: x * 10^dp is exact in x87 long double (53 + at most 10 significant bits
+// of 5^dp <= 64), rintl rounds that exact value half-even like printf does, and for |n| < 2^53 the
+// quotient n / 10^dp is the double nearest the decimal n·10^-dp, which is what strtod returns.
+inline bool round_fast(double x, int dp, double* y) {
+    static const long double kP10[5] = {1.0L, 10.0L, 100.0L, 1000.0L, 10000.0L};
+    if (dp > 4 || !std::isfinite(x)) return false;
+    long double prod = (long double)x * kP10[dp];
+    if (!(std::fabs(prod) < 9007199254740992.0L)) return false;
+    long double n = rintl(prod);
+    *y = (double)n / (double)kP10[dp];
+    return true;
+}
+
 inline int py_round_float(double x, int dp, char* out) {
     double y = x;
+    if (round_fast(x, dp, &y)) return py_repr(y, out);
     if (std::isfinite(x) && dp <= 323) {
         char b[400];
         std::snprintf(b, sizeof b, "%.*f", dp, x);
@@ -784,6 +798,47 @@ inline int py_int(int64_t v, char* out) {
     auto r = std::to_chars(out, out + 24, v);
     *r.ptr = 0;
     return (int)(r.ptr - out);
+}
+
+inline char* put_int(char* w, int64_t v) { return std::to_chars(w, w + 24, v).ptr; }
+
+inline char* put_str(char* w, const char* s, size_t n) {
+    std::memcpy(w, s, n);
+    return w + n;
+}
+
+// str(round(x, dp)) written at w.  With dp <= 4 and |n| < 10^15 (n = x·10^dp rounded, see
+// round_fast) the decimal n·10^-dp has <= 15 significant digits, so it is the only decimal of
+// that length mapping to the rounded double and repr() prints exactly it (trailing zeros
+// stripped, ".0" if integral; fixed notation since 1e-4 <= |y| < 1e16 or y == 0).
+inline char* put_round(char* w, double x, int dp) {
+    static const long double kP10[5] = {1.0L, 10.0L, 100.0L, 1000.0L, 10000.0L};
+    static const int64_t kI10[5] = {1, 10, 100, 1000, 10000};
+    if (dp <= 4 && std::isfinite(x)) {
+        long double r = rintl((long double)x * kP10[dp]);
+        if (std::fabs(r) < 1e15L) {
+            if (std::signbit(r)) *w++ = '-';
+            int64_t n = (int64_t)std::fabs(r);
+            w = put_int(w, n / kI10[dp]);
+            *w++ = '.';
+            int64_t fr = n % kI10[dp];
+            if (fr == 0) {
+                *w++ = '0';
+                return w;
+            }
+            int nd = dp;
+            while (fr % 10 == 0) {
+                fr /= 10;
+                --nd;
+            }
+            for (int i = nd - 1; i >= 0; --i) {
+                w[i] = (char)('0' + fr % 10);
+                fr /= 10;
+            }
+            return w + nd;
+        }
+    }
+    return w + py_round_float(x, dp, w);
 }
 
 }  // namespace
@@ -826,16 +881,19 @@ extern "C" int bcio_fmt_rows(bcio_fmt* b, const char* ref, int64_t L, int k, con
     }
     static const char* kBase[6] = {"A", "C", "G", "T", "DS", "N"};
     const std::string refs(ref);
+    const size_t rl = refs.size();
     nthreads = hw_threads(nthreads);
-    const int64_t per = 1 << 14;
+    const int64_t per = std::max<int64_t>(256, std::min<int64_t>(1 << 14, L / (8 * nthreads) + 1));
     const int64_t nchunks = (L + per - 1) / per;
-    std::vector<std::string> parts((size_t)nchunks);
+    // worst case per position: k rows of ref + 4 ints + 3 floats (repr <= 25 chars) + separators
+    const size_t row_max = (size_t)k * (rl + 4 * 24 + 3 * 32 + 16);
+    std::vector<uvec<char>> parts((size_t)nchunks);
     parallel_for(nchunks, nthreads, [&](int64_t c0, int64_t c1) {
-        char tmp[512];
         for (int64_t c = c0; c < c1; ++c) {
-            std::string& s = parts[(size_t)c];
+            uvec<char>& s = parts[(size_t)c];
             const int64_t p0 = c * per, p1 = std::min(L, p0 + per);
-            s.reserve((size_t)(p1 - p0) * (long_format ? 6 * 48 : 96));
+            s.resize((size_t)(p1 - p0) * row_max);
+            char* w = s.data();
             for (int64_t p = p0; p < p1; ++p) {
                 int64_t cov = 0;
                 int nz = 0;
@@ -844,77 +902,66 @@ extern "C" int bcio_fmt_rows(bcio_fmt* b, const char* ref, int64_t L, int k, con
                     nz += counts[(int64_t)j * L + p] != 0;
                 }
                 // entropy / secondary text, shared by all k long rows
-                char et[400], st[400];
-                if (cov == 0) {
-                    std::strcpy(et, "1");
-                    std::strcpy(st, "1");
-                } else {
-                    py_round_float(ent[p], dp, et);
-                    if (nz <= 1)
-                        std::strcpy(st, "1");
-                    else
-                        py_round_float(sec[p], dp, st);
+                char et[64], st[64];
+                size_t etn = 1, stn = 1;
+                et[0] = st[0] = '1';
+                if (cov != 0) {
+                    etn = (size_t)(put_round(et, ent[p], dp) - et);
+                    if (nz > 1) stn = (size_t)(put_round(st, sec[p], dp) - st);
                 }
-                char post[24], covt[24];
-                py_int(p + 1, post);
-                py_int(cov, covt);
+                char head[64];
+                char* h = head;
+                *h++ = '\t';
+                h = put_int(h, p + 1);
+                *h++ = '\t';
+                h = put_int(h, cov);
+                const size_t hn = (size_t)(h - head);
                 if (!long_format) {
-                    s += refs;
-                    s += '\t';
-                    s += post;
-                    s += '\t';
-                    s += covt;
+                    w = put_str(w, refs.data(), rl);
+                    w = put_str(w, head, hn);
                     for (int j = 0; j < k; ++j) {
-                        s += '\t';
-                        py_int(counts[(int64_t)j * L + p], tmp);
-                        s += tmp;
+                        *w++ = '\t';
+                        w = put_int(w, counts[(int64_t)j * L + p]);
                     }
                     for (int j = 0; j < k; ++j) {
-                        s += '\t';
+                        *w++ = '\t';
                         if (cov == 0)
-                            s += "-1";
-                        else {
-                            py_round_float(pc[(int64_t)j * L + p], dp, tmp);
-                            s += tmp;
-                        }
+                            w = put_str(w, "-1", 2);
+                        else
+                            w = put_round(w, pc[(int64_t)j * L + p], dp);
                     }
-                    s += '\t';
-                    s += et;
-                    s += '\t';
-                    s += st;
-                    s += '\n';
+                    *w++ = '\t';
+                    w = put_str(w, et, etn);
+                    *w++ = '\t';
+                    w = put_str(w, st, stn);
+                    *w++ = '\n';
                 } else {
                     for (int j = 0; j < k; ++j) {
-                        s += refs;
-                        s += '\t';
-                        s += post;
-                        s += '\t';
-                        s += covt;
-                        s += '\t';
-                        s += kBase[j];
-                        s += '\t';
-                        py_int(counts[(int64_t)j * L + p], tmp);
-                        s += tmp;
-                        s += '\t';
+                        w = put_str(w, refs.data(), rl);
+                        w = put_str(w, head, hn);
+                        *w++ = '\t';
+                        w = put_str(w, kBase[j], j == 4 ? 2 : 1);
+                        *w++ = '\t';
+                        w = put_int(w, counts[(int64_t)j * L + p]);
+                        *w++ = '\t';
                         if (cov == 0)
-                            s += "-1";
-                        else {
-                            py_round_float(pc[(int64_t)j * L + p], dp, tmp);
-                            s += tmp;
-                        }
-                        s += '\t';
-                        s += et;
-                        s += '\t';
-                        s += st;
-                        s += '\n';
+                            w = put_str(w, "-1", 2);
+                        else
+                            w = put_round(w, pc[(int64_t)j * L + p], dp);
+                        *w++ = '\t';
+                        w = put_str(w, et, etn);
+                        *w++ = '\t';
+                        w = put_str(w, st, stn);
+                        *w++ = '\n';
                     }
                 }
             }
+            s.resize((size_t)(w - s.data()));
         }
     });
     size_t tot = b->buf.size();
     for (auto& s : parts) tot += s.size();
     b->buf.reserve(tot);
-    for (auto& s : parts) b->buf += s;
+    for (auto& s : parts) b->buf.append(s.data(), s.size());
     return BCIO_OK;
 }

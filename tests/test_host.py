@@ -182,3 +182,19 @@ def test_bam_corrupt_block(tmp_path):
     open(path, "wb").write(bytes(data))
     with pytest.raises(Exception):
         BamFile(path)
+
+
+@pytest.mark.parametrize("dp", [0, 1, 2, 3, 4, 5])
+def test_pyround_native_decimal_ties(dp):
+    """Values at and next to decimal ties (k + 1/2)·10^-dp, whose binary value sits just above or
+    below the tie: the long-double fast path (dp <= 4) and printf/strtod (dp > 4) both match
+    CPython's round()."""
+    rng = np.random.default_rng(dp)
+    ks = rng.integers(0, 10 ** 7, 3000)
+    xs = []
+    for kk in ks:
+        t = (int(kk) + 0.5) / 10 ** dp
+        xs += [t, np.nextafter(t, 0.0), np.nextafter(t, 1e300), -t]
+    xs += [float(v) / 8 for v in range(-64, 64)] + [2.0 ** 52 + 0.5, 2.0 ** 53, 4.5e15, 9.5e15]
+    for x in xs:
+        assert fmt.pyround_native(float(x), dp) == str(round(float(x), dp)), (x, dp)

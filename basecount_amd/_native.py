@@ -49,6 +49,7 @@ class BcioRecords(C.Structure):
         ("seq", C.c_void_p),
         ("qual", C.c_void_p),
         ("seq_bytes", C.c_uint64),
+        ("ref_span", C.c_void_p),
     ]
 
 
@@ -65,6 +66,7 @@ class BcioSelection(C.Structure):
         ("qlen", C.c_void_p),
         ("ordinal", C.c_void_p),
         ("rec", C.c_void_p),
+        ("span", C.c_void_p),
     ]
 
 

@@ -35,7 +35,9 @@ SEQ_NT16 = "=ACMGRSVTWYHKDBN"
 
 @dataclass
 class Selection:
-    """Accepted reads of the requested references (flat arrays sliced by ``ref_beg``)."""
+    """Accepted reads of the requested references (flat arrays sliced by ``ref_beg``).  Like the
+    record arrays of BamFile, these are views of the decoder's memory (each select() call gets
+    its own block): valid until the BamFile is closed."""
 
     n_accepted: int
     keyerror_ordinal: int
@@ -48,6 +50,7 @@ class Selection:
     qlen: np.ndarray
     ordinal: np.ndarray
     rec: np.ndarray
+    span: np.ndarray  # int64 reference span (M/D/N/=/X) of each selected read
 
 
 class BamFile:
@@ -81,6 +84,7 @@ class BamFile:
         self.seq_off = _view(r.seq_off, n + 1, np.uint64)
         self.seq = _view(r.seq, int(r.seq_bytes), np.uint8)
         self.qual = _view(r.qual, 2 * int(r.seq_bytes), np.uint8)
+        self.ref_span = _view(r.ref_span, n, np.int64)
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -117,13 +121,14 @@ class BamFile:
             keyerror_ordinal=int(o.keyerror_ordinal),
             keyerror_rec=int(o.keyerror_rec),
             ref_beg=ref_beg,
-            pos=_view(o.pos, m, np.int32).copy(),
-            cig_beg=_view(o.cig_beg, m, np.uint32).copy(),
-            cig_n=_view(o.cig_n, m, np.uint32).copy(),
-            seq_nib=_view(o.seq_nib, m, np.uint32).copy(),
-            qlen=_view(o.qlen, m, np.uint32).copy(),
-            ordinal=_view(o.ordinal, m, np.int64).copy(),
-            rec=_view(o.rec, m, np.int64).copy(),
+            pos=_view(o.pos, m, np.int32),
+            cig_beg=_view(o.cig_beg, m, np.uint32),
+            cig_n=_view(o.cig_n, m, np.uint32),
+            seq_nib=_view(o.seq_nib, m, np.uint32),
+            qlen=_view(o.qlen, m, np.uint32),
+            ordinal=_view(o.ordinal, m, np.int64),
+            rec=_view(o.rec, m, np.int64),
+            span=_view(o.span, m, np.int64),
         )
 
     # ---- pysam-like per-record accessors (tests / oracle shim only; slow) -------------------

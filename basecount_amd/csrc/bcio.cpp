@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <memory>
 #include <string>
 #include <thread>
 #include <utility>
@@ -194,16 +195,21 @@ struct bcio_file {
     std::vector<int64_t> lens;
     // raw SoA
     uvec<int32_t> tid, pos, l_seq, qstart, qend;
+    uvec<int64_t> ref_span;
     uvec<uint16_t> flag;
     uvec<uint8_t> mapq;
     uvec<uint32_t> rec_err;
     uvec<uint64_t> cig_off, seq_off;
     uvec<uint32_t> cigar;
     uvec<uint8_t> seq, qual;
-    // selection outputs
-    std::vector<int64_t> s_ref_beg, s_ordinal, s_rec;
-    std::vector<int32_t> s_pos;
-    std::vector<uint32_t> s_cig_beg, s_cig_n, s_seq_nib, s_qlen;
+    // selection outputs: one block per bcio_select call, alive until bcio_close
+    struct Sel {
+        std::vector<int64_t> ref_beg;
+        uvec<int64_t> ordinal, rec, span;
+        uvec<int32_t> pos;
+        uvec<uint32_t> cig_beg, cig_n, seq_nib, qlen;
+    };
+    std::vector<std::unique_ptr<Sel>> sels;
 };
 
 extern "C" const char* bcio_last_error(void) { return g_err.c_str(); }
@@ -444,6 +450,7 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
     f->l_seq.resize(n);
     f->qstart.resize(n);
     f->qend.resize(n);
+    f->ref_span.resize(n);
     f->flag.resize(n);
     f->mapq.resize(n);
     f->rec_err.resize(n);
@@ -473,7 +480,13 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
             f->l_seq[i] = ls;
             const uint8_t* c = r + 32 + lrn;
             uint32_t* cd = f->cigar.data() + f->cig_off[i];
-            for (uint16_t k = 0; k < nc; ++k) cd[k] = rd32(c + 4 * k);
+            int64_t span = 0;  // reference-consuming ops M D N = X
+            for (uint16_t k = 0; k < nc; ++k) {
+                uint32_t w = rd32(c + 4 * k);
+                cd[k] = w;
+                if ((0x18Du >> (w & 0xf)) & 1) span += w >> 4;
+            }
+            f->ref_span[i] = span;
             const uint8_t* s = c + 4ull * nc;
             uint64_t sb = (uint64_t)((ls + 1) / 2);
             std::memcpy(f->seq.data() + f->seq_off[i], s, sb);
@@ -526,68 +539,109 @@ extern "C" int bcio_get_records(const bcio_file* f, bcio_records* o) {
     o->seq = f->seq.data();
     o->qual = f->qual.data();
     o->seq_bytes = f->seq_off.empty() ? 0 : f->seq_off.back();
+    o->ref_span = f->ref_span.data();
     return BCIO_OK;
 }
 
 extern "C" int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_sel, bcio_selection* o) {
     if (!f || !o || !ref_sel) return fail(BCIO_E_ARG, "null argument");
+    f->sels.emplace_back(new bcio_file::Sel());
+    bcio_file::Sel& S = *f->sels.back();
     const int64_t n = (int64_t)f->tid.size();
     const int32_t nr = (int32_t)f->names.size();
-    std::vector<int64_t> cnt(nr + 1, 0);
-    int64_t ordinal = 0;
+    // accepted = mapped and mapq >= mmq (main.py:165); is_unmapped is flag bit 4 only.
+    // Two parallel passes over fixed record chunks: count per (chunk, reference), then scatter
+    // at offsets that keep file order within each reference.
+    auto accepted = [&](int64_t i) { return !(f->flag[i] & 4) && (int64_t)f->mapq[i] >= min_mapq; };
+    auto wanted = [&](int32_t t) { return t >= 0 && t < nr && ref_sel[t]; };
+    const int64_t per = 1 << 16;
+    const int64_t nch = (n + per - 1) / per;
+    const int cols = nr + 1;  // per-reference counts + accepted ordinals of the chunk
+    std::vector<int64_t> cc((size_t)(nch * cols), 0);
+    std::vector<int64_t> ke_rec((size_t)nch, -1), ke_ord((size_t)nch, -1);
+    const int nthreads = hw_threads(0);
+    parallel_for(nch, nthreads, [&](int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; ++c) {
+            int64_t* row = &cc[(size_t)(c * cols)];
+            int64_t ord = 0;
+            for (int64_t i = c * per, e = std::min(n, i + per); i < e; ++i) {
+                if (!accepted(i)) continue;
+                int32_t t = f->tid[i];
+                if (wanted(t))
+                    row[t]++;
+                else if (ke_rec[c] < 0) {
+                    ke_rec[c] = i;
+                    ke_ord[c] = ord;
+                }
+                ord++;
+            }
+            row[nr] = ord;
+        }
+    });
+    S.ref_beg.assign(nr + 1, 0);
+    for (int64_t c = 0; c < nch; ++c)
+        for (int32_t t = 0; t < nr; ++t) S.ref_beg[t + 1] += cc[(size_t)(c * cols + t)];
+    for (int32_t t = 0; t < nr; ++t) S.ref_beg[t + 1] += S.ref_beg[t];
+    // chunk c's first slot per reference, and its first ordinal
+    std::vector<int64_t> ord0((size_t)nch + 1, 0);
+    std::vector<int64_t> run(S.ref_beg.begin(), S.ref_beg.end() - 1);
     o->keyerror_ordinal = -1;
     o->keyerror_rec = -1;
-    // accepted = mapped and mapq >= mmq (main.py:165); is_unmapped is flag bit 4 only.
-    for (int64_t i = 0; i < n; ++i) {
-        if ((f->flag[i] & 4) || (int64_t)f->mapq[i] < min_mapq) continue;
-        int32_t t = f->tid[i];
-        if (t < 0 || t >= nr || !ref_sel[t]) {
-            if (o->keyerror_ordinal < 0) {
-                o->keyerror_ordinal = ordinal;
-                o->keyerror_rec = i;
+    for (int64_t c = 0; c < nch; ++c) {
+        int64_t* row = &cc[(size_t)(c * cols)];
+        for (int32_t t = 0; t < nr; ++t) {
+            int64_t k = row[t];
+            row[t] = run[t];
+            run[t] += k;
+        }
+        if (o->keyerror_rec < 0 && ke_rec[c] >= 0) {
+            o->keyerror_rec = ke_rec[c];
+            o->keyerror_ordinal = ord0[c] + ke_ord[c];
+        }
+        ord0[c + 1] = ord0[c] + row[nr];
+    }
+    o->n_accepted = ord0[nch];
+    const int64_t m = S.ref_beg[nr];
+    S.pos.resize(m);
+    S.cig_beg.resize(m);
+    S.cig_n.resize(m);
+    S.seq_nib.resize(m);
+    S.qlen.resize(m);
+    S.ordinal.resize(m);
+    S.rec.resize(m);
+    S.span.resize(m);
+    parallel_for(nch, nthreads, [&](int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; ++c) {
+            int64_t* slot = &cc[(size_t)(c * cols)];
+            int64_t ordinal = ord0[c];
+            for (int64_t i = c * per, e = std::min(n, i + per); i < e; ++i) {
+                if (!accepted(i)) continue;
+                int32_t t = f->tid[i];
+                if (wanted(t)) {
+                    int64_t j = slot[t]++;
+                    S.pos[j] = f->pos[i];
+                    S.cig_beg[j] = (uint32_t)f->cig_off[i];
+                    S.cig_n[j] = (uint32_t)(f->cig_off[i + 1] - f->cig_off[i]);
+                    S.seq_nib[j] = (uint32_t)(2 * f->seq_off[i] + (uint64_t)std::max(0, f->qstart[i]));
+                    int32_t ql = f->qend[i] - f->qstart[i];
+                    S.qlen[j] = (uint32_t)std::max(0, ql);
+                    S.ordinal[j] = ordinal;
+                    S.rec[j] = i;
+                    S.span[j] = f->ref_span[i];
+                }
+                ordinal++;
             }
-        } else {
-            cnt[t + 1]++;
         }
-        ordinal++;
-    }
-    o->n_accepted = ordinal;
-    f->s_ref_beg.assign(nr + 1, 0);
-    for (int32_t t = 0; t < nr; ++t) f->s_ref_beg[t + 1] = f->s_ref_beg[t] + cnt[t + 1];
-    const int64_t m = f->s_ref_beg[nr];
-    f->s_pos.resize(m);
-    f->s_cig_beg.resize(m);
-    f->s_cig_n.resize(m);
-    f->s_seq_nib.resize(m);
-    f->s_qlen.resize(m);
-    f->s_ordinal.resize(m);
-    f->s_rec.resize(m);
-    std::vector<int64_t> fill(f->s_ref_beg.begin(), f->s_ref_beg.end() - 1);
-    ordinal = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        if ((f->flag[i] & 4) || (int64_t)f->mapq[i] < min_mapq) continue;
-        int32_t t = f->tid[i];
-        if (t >= 0 && t < nr && ref_sel[t]) {
-            int64_t j = fill[t]++;
-            f->s_pos[j] = f->pos[i];
-            f->s_cig_beg[j] = (uint32_t)f->cig_off[i];
-            f->s_cig_n[j] = (uint32_t)(f->cig_off[i + 1] - f->cig_off[i]);
-            f->s_seq_nib[j] = (uint32_t)(2 * f->seq_off[i] + (uint64_t)std::max(0, f->qstart[i]));
-            int32_t ql = f->qend[i] - f->qstart[i];
-            f->s_qlen[j] = (uint32_t)std::max(0, ql);
-            f->s_ordinal[j] = ordinal;
-            f->s_rec[j] = i;
-        }
-        ordinal++;
-    }
-    o->ref_beg = f->s_ref_beg.data();
-    o->pos = f->s_pos.data();
-    o->cig_beg = f->s_cig_beg.data();
-    o->cig_n = f->s_cig_n.data();
-    o->seq_nib = f->s_seq_nib.data();
-    o->qlen = f->s_qlen.data();
-    o->ordinal = f->s_ordinal.data();
-    o->rec = f->s_rec.data();
+    });
+    o->ref_beg = S.ref_beg.data();
+    o->pos = S.pos.data();
+    o->cig_beg = S.cig_beg.data();
+    o->cig_n = S.cig_n.data();
+    o->seq_nib = S.seq_nib.data();
+    o->qlen = S.qlen.data();
+    o->ordinal = S.ordinal.data();
+    o->rec = S.rec.data();
+    o->span = S.span.data();
     if (f->cig_off.back() > 0xFFFFFFFFull || 2 * f->seq_off.back() > 0xFFFFFFFFull)
         return fail(BCIO_E_ARG, "file too large for 32-bit batch offsets; split it");
     return BCIO_OK;

@@ -326,14 +326,8 @@ class _FileOnDevice:
         self.cig_n = np.where(faulty, 0, sel.cig_n).astype(np.uint32)
         self.pos = np.where(faulty, 0, sel.pos).astype(np.int32)
         self.sel = sel
-        # reference spans per record (for the LDS window bound)
-        op = f.cigar & 0xF
-        ln = (f.cigar >> 4).astype(np.int64)
-        cons = (op == 0) | (op == 2) | (op == 3) | (op == 7) | (op == 8)
-        csum = np.zeros(f.cigar.size + 1, np.int64)
-        np.cumsum(np.where(cons, ln, 0), out=csum[1:])
-        span = csum[f.cig_off[1:].astype(np.int64)] - csum[f.cig_off[:-1].astype(np.int64)]
-        self.span = np.where(faulty, 0, span[sel.rec]) if sel.rec.size else np.zeros(0, np.int64)
+        # reference spans per read (for the LDS window bound), from the decoder
+        self.span = np.where(faulty, 0, sel.span)
         self.d_cigar = ctx.alloc(max(4, f.cigar.nbytes)).upload(f.cigar)
         # packed SEQ in the kernels' layout (BC_SEQ_EVENT), converted in place on the device
         self.d_seq = ctx.alloc(D.seq_event_bytes(f.seq.nbytes)).upload(f.seq)

@@ -58,6 +58,7 @@ typedef struct bcio_records {
     const uint8_t* qual;    /* QUAL laid out by NIBBLE index: base i of record r is at
                                qual[2*seq_off[r] + i]  (so one offset addresses both)         */
     uint64_t seq_bytes;     /* = seq_off[n]                                                   */
+    const int64_t* ref_span;/* [n] reference span: sum of M/D/N/=/X lengths                     */
 } bcio_records;
 
 /* Open and fully decode a BAM file with `nthreads` inflate/decode threads (<=0: hardware). */
@@ -91,6 +92,7 @@ typedef struct bcio_selection {
     const uint32_t* qlen;
     const int64_t* ordinal;
     const int64_t* rec;
+    const int64_t* span;          /* ref_span[rec[i]]                                           */
 } bcio_selection;
 
 int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_sel, bcio_selection* out);

@@ -38,6 +38,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--summarise", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="cProfile get_basecounts (stderr)")
     args = ap.parse_args()
     rs = synth.make_config(args.config)
     tmp = tempfile.mkdtemp(prefix="bc_e2e_")
@@ -53,6 +54,14 @@ def main():
 
     mode = "summary" if args.summarise else "rows"
     res["get_basecounts_s"], data = _t(lambda: M.get_basecounts(bam, _mode=mode))
+    if args.profile:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        M.get_basecounts(bam, _mode=mode)
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
 
     if not args.summarise:
         def format_all():

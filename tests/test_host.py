@@ -198,3 +198,31 @@ def test_pyround_native_decimal_ties(dp):
     xs += [float(v) / 8 for v in range(-64, 64)] + [2.0 ** 52 + 0.5, 2.0 ** 53, 4.5e15, 9.5e15]
     for x in xs:
         assert fmt.pyround_native(float(x), dp) == str(round(float(x), dp)), (x, dp)
+
+
+def test_select_multi_chunk(tmp_path):
+    """The parallel selection (65,536-record chunks) keeps file order per reference, the global
+    accepted ordinals, the first KeyError read (main.py:166) and the decoder's reference spans."""
+    rs = synth.make_reads([("a", 40_000), ("b", 30_000), ("c", 20_000)], 60_000, True, 31)
+    rs.flag[::7] |= 4
+    path = str(tmp_path / "big.bam")
+    synth.write_bam(rs, path)
+    with BamFile(path) as f:
+        ops, lens = f.cigar & 15, (f.cigar >> 4).astype(np.int64)
+        cons = np.isin(ops, [0, 2, 3, 7, 8])
+        rec_of = np.repeat(np.arange(f.n_records), np.diff(f.cig_off).astype(np.int64))
+        span = np.bincount(rec_of, weights=np.where(cons, lens, 0), minlength=f.n_records)
+        assert np.array_equal(f.ref_span, span.astype(np.int64))
+        for mmq in (0, 31):
+            sel = f.select(mmq, [True, False, True])
+            acc = ((rs.flag & 4) == 0) & (rs.mapq >= mmq)
+            ordinal = np.cumsum(acc) - 1
+            keep = acc & np.isin(rs.tid, [0, 2])
+            idx = np.nonzero(keep)[0]
+            idx = idx[np.argsort(rs.tid[idx], kind="stable")]
+            assert np.array_equal(sel.rec, idx)
+            assert np.array_equal(sel.ordinal, ordinal[idx])
+            assert np.array_equal(sel.span, span[idx].astype(np.int64))
+            assert sel.n_accepted == int(acc.sum())
+            bad = np.nonzero(acc & (rs.tid == 1))[0]
+            assert sel.keyerror_rec == bad[0] and sel.keyerror_ordinal == ordinal[bad[0]]

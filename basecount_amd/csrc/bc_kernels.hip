@@ -468,21 +468,39 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const do
     }
 }
 
-__global__ void k_sum_final(const double* part_ent, const long long* part_cov, const long long* part_nz,
-                            int64_t nchunks, int64_t L, double* out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// One workgroup: the float64 fold over the per-buffer partials stays sequential (numpy adds the
+// buffers' pairwise sums in order), but 256 partials at a time are staged through LDS by the
+// whole block so thread 0 folds from LDS instead of waiting on one global load per buffer; the
+// integer sums are order-free and reduce in parallel.
+__global__ __launch_bounds__(256) void k_sum_final(const double* part_ent, const long long* part_cov,
+                                                   const long long* part_nz, int64_t nchunks, int64_t L,
+                                                   double* out) {
+    __shared__ double s_buf[256];
+    __shared__ long long s_red[4];
     double s = 0.0;
     long long cs = 0, nz = 0;
-    for (int64_t c = 0; c < nchunks; ++c) {
-        s += part_ent[c];
-        cs += part_cov[c];
-        nz += part_nz[c];
+    for (int64_t c0 = 0; c0 < nchunks; c0 += 256) {
+        const int64_t c = c0 + threadIdx.x;
+        const int m = (int)((nchunks - c0) < 256 ? (nchunks - c0) : 256);
+        if (c < nchunks) {
+            s_buf[threadIdx.x] = part_ent[c];
+            cs += part_cov[c];
+            nz += part_nz[c];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < m; ++i) s += s_buf[i];
+        __syncthreads();
     }
-    const double n = (double)L;
-    out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
-    out[1] = s / n;
-    out[2] = (double)nz;
-    out[3] = (double)cs;
+    cs = block_sum_i64(cs, s_red);
+    nz = block_sum_i64(nz, s_red);
+    if (threadIdx.x == 0) {
+        const double n = (double)L;
+        out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
+        out[1] = s / n;
+        out[2] = (double)nz;
+        out[3] = (double)cs;
+    }
 }
 
 // ------------------------------------------------------------------------------ amplicons
@@ -655,7 +673,7 @@ hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, 
     long long* pcv = (long long*)(pe + (nc > 0 ? nc : 1));
     long long* pnz = pcv + (nc > 0 ? nc : 1);
     if (nc > 0) hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)nc), dim3(256), 0, s, cov, ent, L, pe, pcv, pnz);
-    hipLaunchKernelGGL(k_sum_final, dim3(1), dim3(64), 0, s, pe, pcv, pnz, nc, L, out);
+    hipLaunchKernelGGL(k_sum_final, dim3(1), dim3(256), 0, s, pe, pcv, pnz, nc, L, out);
     return hipGetLastError();
 }
 

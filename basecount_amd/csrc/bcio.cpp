@@ -513,7 +513,16 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
     return BCIO_OK;
 }
 
-extern "C" void bcio_close(bcio_file* f) { delete f; }
+// Returning a few hundred MB of decoded arrays to the kernel takes tens of ms; nothing waits for
+// it, so it happens on a detached thread (synchronously if a thread cannot be started).
+extern "C" void bcio_close(bcio_file* f) {
+    if (!f) return;
+    try {
+        std::thread([f] { delete f; }).detach();
+    } catch (...) {
+        delete f;
+    }
+}
 extern "C" int32_t bcio_n_refs(const bcio_file* f) { return f ? (int32_t)f->names.size() : 0; }
 extern "C" const char* bcio_ref_name(const bcio_file* f, int32_t i) {
     return (f && i >= 0 && i < (int32_t)f->names.size()) ? f->names[i].c_str() : nullptr;

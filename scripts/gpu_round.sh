@@ -20,6 +20,8 @@ for s in $STEPS; do
     tests) run tests 1200 python -m pytest tests -m gpu -x -q -s ${PYTEST_ARGS} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS} ;;
     bench3) run bench3 600 python bench.py --config c3 --no-cpu-baseline ${BENCH_ARGS} ;;
+    bench5) run bench5 600 python bench.py --config c5 --no-cpu-baseline --steps 10 --warmup 2 ${BENCH_ARGS} ;;
+    e2e)   run e2e 900 bash -c "python scripts/e2e.py --config c2 && python scripts/e2e.py --config c3 && python scripts/e2e.py --config c5 --summarise" ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --steps 200 ${BENCH_ARGS} ;;
     prof5) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null

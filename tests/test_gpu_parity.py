@@ -222,7 +222,7 @@ def test_kernel2_matches_oracle(ctx, show_n):
 
 
 @pytest.mark.parametrize("L", [1, 7, 8, 9, 127, 128, 129, 136, 1000, 8191, 8192, 8193, 29_903,
-                               100_000, 1_000_003])
+                               100_000, 1_000_003, 2_203_000, 6_000_001])
 def test_summary_matches_numpy(ctx, L):
     rng = np.random.default_rng(L)
     cov = rng.integers(0, 5000, L).astype(np.int32)

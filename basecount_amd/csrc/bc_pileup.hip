@@ -86,36 +86,46 @@ __device__ __forceinline__ uint32_t resolve_slow(int j, int jlo, uint32_t cn, ui
 }
 
 // First indices with pos >= v_lo (lanes 0-31) and pos >= v_hi (lanes 32-63), searched together:
-// 32 probes per half-wave per round.  Returns {lower_bound(v_lo), lower_bound(v_hi)}.
-__device__ __forceinline__ void lower_bound_pair(const int32_t* pos, int64_t n, int64_t v_lo, int64_t v_hi, int lane,
-                                                 int64_t& r_lo, int64_t& r_hi) {
+// 32 probes per half-wave per round.  Returns {lower_bound(v_lo), lower_bound(v_hi)}.  IT: the
+// index arithmetic (uint32_t for batches of < 2^31 reads: the rounds are mostly 64-bit VALU
+// otherwise).
+template <typename IT>
+__device__ __forceinline__ void lower_bound_pair_t(const int32_t* pos, IT n, int64_t v_lo, int64_t v_hi, int lane,
+                                                   int64_t& r_lo, int64_t& r_hi) {
     const int h = lane >> 5, l = lane & 31;
     const int64_t v = h ? v_hi : v_lo;
-    int64_t lo = 0, hi = n;  // answer in [lo, hi] (per half)
+    IT lo = 0, hi = n;  // answer in [lo, hi] (per half)
     while (__any(hi - lo > 32)) {
         const bool act = hi - lo > 32;
-        const int64_t s = act ? ((hi - lo) / 33 > 0 ? (hi - lo) / 33 : 1) : 1;
-        const int64_t idx = lo + (int64_t)(l + 1) * s;
+        const IT s = act ? ((hi - lo) / 33 > 0 ? (hi - lo) / 33 : 1) : 1;
+        const IT idx = lo + (IT)(l + 1) * s;
         const bool less = act && idx < hi && (int64_t)pos[idx] < v;
         const unsigned long long m = __ballot(less);
-        const int c = __popc(h ? (unsigned)(m >> 32) : (unsigned)m);
+        const IT c = (IT)__popc(h ? (unsigned)(m >> 32) : (unsigned)m);
         if (act) {
-            const int64_t nlo = c ? lo + (int64_t)c * s + 1 : lo;
-            const int64_t nhi = (c < 32 && lo + (int64_t)(c + 1) * s < hi) ? lo + (int64_t)(c + 1) * s : hi;
+            const IT nlo = c ? lo + c * s + 1 : lo;
+            const IT nhi = (c < 32 && lo + (c + 1) * s < hi) ? lo + (c + 1) * s : hi;
             lo = nlo;
             hi = nhi;
         }
     }
-    const int64_t idx = lo + l;
+    const IT idx = lo + (IT)l;
     const bool less = idx < hi && (int64_t)pos[idx] < v;
     const unsigned long long m = __ballot(less);
-    const int64_t res = lo + __popc(h ? (unsigned)(m >> 32) : (unsigned)m);
+    const int64_t res = (int64_t)lo + __popc(h ? (unsigned)(m >> 32) : (unsigned)m);
     // wave-uniform results (SGPRs): the chunk loops over [r_lo, r_hi) stay scalar
     const uint32_t rl = (uint32_t)res, rh = (uint32_t)((uint64_t)res >> 32);
     r_lo = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rh, 0) << 32) |
                      (uint32_t)__builtin_amdgcn_readlane((int)rl, 0));
     r_hi = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rh, 32) << 32) |
                      (uint32_t)__builtin_amdgcn_readlane((int)rl, 32));
+}
+__device__ __forceinline__ void lower_bound_pair(const int32_t* pos, int64_t n, int64_t v_lo, int64_t v_hi, int lane,
+                                                 int64_t& r_lo, int64_t& r_hi) {
+    if (n < (int64_t)0x7FFFFFC0)
+        lower_bound_pair_t<uint32_t>(pos, (uint32_t)n, v_lo, v_hi, lane, r_lo, r_hi);
+    else
+        lower_bound_pair_t<int64_t>(pos, n, v_lo, v_hi, lane, r_lo, r_hi);
 }
 
 __device__ __forceinline__ void flush_acc(unsigned long long& acc, uint32_t (&cnt)[6]) {
@@ -155,7 +165,10 @@ __device__ __attribute__((noinline)) void tile_terms(const PileArgs& A, const ui
                                                      int64_t t0, int first, int stride) {
     const int64_t L = A.L;
     for (int slot = first; slot < 2 * K * kTile; slot += stride) {
-        const int sc = slot / kTile, p = slot % kTile;
+        // slot order A C G T, A2 C2 G2 T2, DS DS2 [N N2]: the deletion / N columns, zero in most
+        // batches, fall in the last (partial) round of the group's lanes
+        const int q = slot / kTile, p = slot % kTile;
+        const int sc = q < 4 ? q : (q < 8 ? K + q - 4 : 4 + ((q - 8) >> 1) + ((q - 8) & 1) * K);
         const int64_t Pp = t0 + p;
         if (Pp >= L) continue;
         uint32_t c[6];
@@ -170,9 +183,13 @@ __device__ __attribute__((noinline)) void tile_terms(const PileArgs& A, const ui
         double term = 0.0;
         if (sc < K) {
             if (cov != 0) {
-                const double pj = (double)c[sc] / (double)cov;
-                if (A.pc) A.pc[(int64_t)sc * L + Pp] = 100.0 * pj;
-                if (c[sc] != 0) term = -(pj * log2(pj));
+                if (c[sc] != 0) {
+                    const double pj = (double)c[sc] / (double)cov;
+                    if (A.pc) A.pc[(int64_t)sc * L + Pp] = 100.0 * pj;
+                    term = -(pj * log2(pj));
+                } else if (A.pc) {
+                    A.pc[(int64_t)sc * L + Pp] = 0.0;  // 100 * (0 / cov), exactly
+                }
             } else if (A.pc) {
                 A.pc[(int64_t)sc * L + Pp] = -1.0;
             }
@@ -271,19 +288,77 @@ __host__ __device__ inline size_t pileup_lds_bytes(int nw, int groups) {
     return (size_t)nw * (kRecBytes + kStageRegion) + kFinBytes;
 }
 
-// One chunk of nr <= 64 reads [base, base + nr) of a tile, walked by one wave: load the reads'
-// fields, decode their CIGARs, stage their sequence into the wave's LDS region and walk them
-// (SWAR windows, or the per-position CIGAR walk for complex reads).  Counts accumulate in W /
-// cnt (lane = tile position t0 + lane), the first out-of-range read in `bad`.
+// Per-read fields of a chunk (lane = read), loaded one chunk ahead of their use.
+struct ReadFields {
+    uint32_t pos, cb, cn, sn;
+};
+__device__ __forceinline__ ReadFields load_fields(const PileArgs& A, int64_t base, int nr, int lane) {
+    ReadFields f{0u, 0u, 0u, 0u};
+    if (lane < nr) {
+        const int64_t r = base + lane;
+        f.pos = (uint32_t)A.pos[r];
+        f.cb = A.cig_beg[r];
+        f.cn = A.cig_n[r];
+        f.sn = A.seq_nib[r];
+    }
+    return f;
+}
+
+// Copy [lo, hi) of the BC_SEQ_EVENT buffer into the wave's stage with register loads, clearing the
+// bases below min_base_quality (count.cpp:56).  Used with a quality threshold only (LDS-DMA
+// cannot apply the mask).
+template <bool QUAL>
+__device__ __forceinline__ void stage_regs(const PileArgs& A, uint8_t* mystage, uint32_t seg_lo, uint32_t seg_hi,
+                                           int lane, bool qual_vec) {
+    for (uint32_t off = lane * 16u; off < seg_hi - seg_lo; off += 1024u) {
+        uint4 v = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
+        if (QUAL) {
+            const int64_t q0 = 2 * ((int64_t)seg_lo + off);  // first base of the piece
+            uint32_t qw[8];
+            if (qual_vec && q0 + 32 <= A.qual_bytes) {
+                const uint4 qa = *(const uint4*)(A.qual + q0), qb = *(const uint4*)(A.qual + q0 + 16);
+                qw[0] = qa.x, qw[1] = qa.y, qw[2] = qa.z, qw[3] = qa.w;
+                qw[4] = qb.x, qw[5] = qb.y, qw[6] = qb.z, qw[7] = qb.w;
+            } else {
+                for (int i = 0; i < 8; ++i) {
+                    qw[i] = 0;
+                    for (int bb = 0; bb < 4; ++bb) {
+                        const int64_t at = q0 + 4 * i + bb;
+                        if (at < A.qual_bytes) qw[i] |= (uint32_t)A.qual[at] << (8 * bb);
+                    }
+                }
+            }
+            v.x &= qual_nibmask(qw[0], qw[1], A.mbq);
+            v.y &= qual_nibmask(qw[2], qw[3], A.mbq);
+            v.z &= qual_nibmask(qw[4], qw[5], A.mbq);
+            v.w &= qual_nibmask(qw[6], qw[7], A.mbq);
+        }
+        *(uint4*)(mystage + off) = v;
+    }
+}
+
+constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's first base
+
+// One chunk of nr <= 64 reads [base, base + nr) of a tile, walked by one wave: decode the reads'
+// CIGARs (fields F were loaded one chunk ahead), stage their sequence into the wave's LDS region
+// and walk them (SWAR windows, or the per-position CIGAR walk for complex reads).  Counts
+// accumulate in W / cnt (lane = tile position t0 + lane), the first out-of-range read in `bad`.
+// On return F holds the fields of the wave's next chunk [next_base, next_base + next_nr),
+// loaded while this chunk is walked.
+//
+// Latency: without a quality threshold the sequence is staged SPECULATIVELY (reads of a sorted
+// batch usually lie in file order: [first read's seq, last read's seq + slack)) by LDS-DMA,
+// issued together with the CIGAR loads, so a chunk costs one memory round trip before its walk;
+// the exact segment, known after the decode, is restaged only when it is not covered.
 template <bool QUAL, int K>
-__device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, int nr, int lane, int s8, int gb,
-                                              int64_t t0, int64_t P, bool edge, bool beyond, uint32_t bmask,
-                                              uint4* myrec, uint8_t* mystage, bool qual_vec, Swar& W, int& it4,
-                                              uint32_t (&cnt)[6], unsigned long long& acc, int& pending,
-                                              int64_t& bad) {
-    // ---- chunk load: per-read fields lane-parallel, CIGAR -> run table (VALU)
+__device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, int nr, ReadFields& F,
+                                              int64_t next_base, int next_nr, int lane, int s8, int gb, int64_t t0,
+                                              int64_t P, bool edge, bool beyond, uint32_t bmask, uint4* myrec,
+                                              uint8_t* mystage, bool qual_vec, Swar& W, int& it4, uint32_t (&cnt)[6],
+                                              unsigned long long& acc, int& pending, int64_t& bad) {
+    // ---- chunk load: CIGAR -> run table (VALU), speculative staging in flight meanwhile
     RunTable T;
-    uint32_t mpos = 0, msn = 0, mcb = 0, mcn = 0;
+    const uint32_t mpos = F.pos, mcb = F.cb, mcn = F.cn, msn = F.sn;
     T.nrun = 0;
     T.complex = false;
     T.gap = false;
@@ -291,29 +366,30 @@ __device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, i
     T.qlen = 0;
 #pragma unroll
     for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
-    if (lane < nr) {
-        const int64_t r = base + lane;
-        mpos = (uint32_t)A.pos[r];
-        mcb = A.cig_beg[r];
-        mcn = A.cig_n[r];
-        msn = A.seq_nib[r];
-    }
     // ops to decode: the wave's largest CIGAR (more than kPre -> complex anyway)
     const int cmax = (int)wave_reduce<true>(mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre);
-    if (lane < nr) {
-        uint32_t w[kPre];
+    uint32_t w[kPre];
 #pragma unroll
-        for (int i = 0; i < kPre; ++i) {
-            w[i] = 0u;
-            if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
-        }
-        T = decode_runs(w, mcn, cmax);
+    for (int i = 0; i < kPre; ++i) {
+        w[i] = 0u;
+        if (lane < nr && i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
     }
+    const bool dma = !QUAL && !(A.ablate & 32);
+    uint32_t spec_lo = 0, spec_hi = 0;
+    bool spec = false;
+    if (dma && !(A.ablate & 512)) {
+        const uint32_t buf_end = (uint32_t)(A.seq_words * 4 < 0xFFFFFFFFll ? A.seq_words * 4 : 0xFFFFFFF0ll);
+        spec_lo = (rdl(msn, 0) >> 1) & ~15u;
+        spec_hi = (rdl(msn, nr - 1) >> 1) + kSpecSlack;
+        spec_hi = spec_hi < buf_end ? spec_hi : buf_end;
+        spec = spec_hi > spec_lo && spec_hi - spec_lo <= (uint32_t)kStage;
+        if (spec) stage_dma<64>(mystage, A.seq + spec_lo, spec_hi - spec_lo, lane);
+    }
+    if (lane < nr) T = decode_runs(w, mcn, cmax);
     const bool cx = __any(T.complex);
     const bool gap = __any(T.gap);
     const int maxrun = (int)wave_reduce<true>((uint32_t)T.nrun);
-    // ---- stage the chunk's sequence (BC_SEQ_EVENT words) into LDS; with a quality
-    // threshold, bases below it are cleared here (count.cpp:56)
+    // ---- the chunk's exact sequence segment (BC_SEQ_EVENT bytes)
     uint32_t blo = 0xFFFFFFFFu, bhi = 0;
     if (lane < nr && T.qlen) {
         blo = msn >> 1;
@@ -322,33 +398,13 @@ __device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, i
     uint32_t seg_lo = wave_reduce<false>(blo);
     const uint32_t seg_hi = wave_reduce<true>(bhi);
     seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
-    const bool staged = !cx && seg_hi - seg_lo <= (uint32_t)kStage && !(A.ablate & 32);
-    if (staged) {
-        for (uint32_t off = lane * 16u; off < seg_hi - seg_lo; off += 1024u) {
-            uint4 v = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
-            if (QUAL) {
-                const int64_t q0 = 2 * ((int64_t)seg_lo + off);  // first base of the piece
-                uint32_t qw[8];
-                if (qual_vec && q0 + 32 <= A.qual_bytes) {
-                    const uint4 qa = *(const uint4*)(A.qual + q0), qb = *(const uint4*)(A.qual + q0 + 16);
-                    qw[0] = qa.x, qw[1] = qa.y, qw[2] = qa.z, qw[3] = qa.w;
-                    qw[4] = qb.x, qw[5] = qb.y, qw[6] = qb.z, qw[7] = qb.w;
-                } else {
-                    for (int i = 0; i < 8; ++i) {
-                        qw[i] = 0;
-                        for (int bb = 0; bb < 4; ++bb) {
-                            const int64_t at = q0 + 4 * i + bb;
-                            if (at < A.qual_bytes) qw[i] |= (uint32_t)A.qual[at] << (8 * bb);
-                        }
-                    }
-                }
-                v.x &= qual_nibmask(qw[0], qw[1], A.mbq);
-                v.y &= qual_nibmask(qw[2], qw[3], A.mbq);
-                v.z &= qual_nibmask(qw[4], qw[5], A.mbq);
-                v.w &= qual_nibmask(qw[6], qw[7], A.mbq);
-            }
-            *(uint4*)(mystage + off) = v;
-        }
+    const bool spec_ok = spec && !cx && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
+    if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
+    const bool staged = !cx && (spec_ok || seg_hi - seg_lo <= (uint32_t)kStage) && !(A.ablate & 32);
+    if (spec && !spec_ok) stage_wait();  // the speculative copy must land before it is overwritten
+    if (staged && !spec_ok) {
+        if (dma) stage_dma<64>(mystage, A.seq + seg_lo, seg_hi - seg_lo, lane);
+        else stage_regs<QUAL>(A, mystage, seg_lo, seg_hi, lane, qual_vec);
     }
     const uint32_t qbase = staged ? 2u * seg_lo : 0u;
     if (cx) {  // walk_complex reads {pos, absolute seq_nib}
@@ -364,6 +420,8 @@ __device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, i
         myrec[lane * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
         myrec[lane * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
     }
+    if (dma) stage_wait();  // LDS-DMA landed (hipcc does not track it)
+    F = load_fields(A, next_base, next_nr, lane);  // in flight during the walk
     __builtin_amdgcn_wave_barrier();
     const int64_t rbase = base;
     if (A.ablate & 4) {
@@ -400,6 +458,7 @@ else BC_WALK(4, GP, ST);                                                        
 template <bool QUAL, int K, bool STATS>
 __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    __shared__ int64_t rng[8][2];  // per group: the tile's read range
     if (A.ablate & 64) return;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -430,9 +489,18 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
         const int gb = (int)t0 + 8 * (lane >> 3);  // this lane's window [gb, gb + 8)
         uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
         int64_t bad = INT64_MAX;
+        // the tile's reads [lo, hi): searched by the group's first wave (the S waves would all
+        // find the same range), handed to the others through LDS
+        int64_t lo = 0, hi = 0;
+        if (ws == 0 && t < A.n_tiles && !(A.ablate & 2))
+            lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
+        if (S > 1) {
+            if (ws == 0 && lane == 0) rng[g][0] = lo, rng[g][1] = hi;
+            __syncthreads();
+            lo = rng[g][0];
+            hi = rng[g][1];
+        }
         if (t < A.n_tiles) {
-            int64_t lo = 0, hi = 0;
-            if (!(A.ablate & 2)) lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
             if (A.ablate & 1) hi = lo;
             const bool edge = t0 + kTile > L;  // uniform
             const bool beyond = P >= L;
@@ -450,10 +518,13 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             int it4 = 0;
             uint4* myrec = rec_all + wave * kTile * 3;
             uint8_t* mystage = stage_all + (size_t)wave * kStageRegion + 16;
-            for (int64_t base = lo + (int64_t)ws * 64; base < hi; base += (int64_t)S * 64) {
-                const int nr = (int)((hi - base) < 64 ? (hi - base) : 64);
-                process_chunk<QUAL, K>(A, base, nr, lane, s8, gb, t0, P, edge, beyond, bmask, myrec, mystage,
-                                       qual_vec, W, it4, cnt, acc, pending, bad);
+            auto chunk_nr = [&](int64_t b) { return b < hi ? (int)((hi - b) < 64 ? (hi - b) : 64) : 0; };
+            int64_t base = lo + (int64_t)ws * 64;
+            ReadFields F = load_fields(A, base, chunk_nr(base), lane);
+            for (; base < hi; base += (int64_t)S * 64) {
+                const int64_t nb = base + (int64_t)S * 64;
+                process_chunk<QUAL, K>(A, base, chunk_nr(base), F, nb, chunk_nr(nb), lane, s8, gb, t0, P, edge,
+                                       beyond, bmask, myrec, mystage, qual_vec, W, it4, cnt, acc, pending, bad);
                 __builtin_amdgcn_wave_barrier();
             }
             flush_acc(acc, cnt);
@@ -644,10 +715,11 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
 #pragma unroll
             for (int c = 0; c < 6; ++c) W.a4[c] = 0;
             int it4 = 0;
+            auto chunk_nr = [&](int64_t b) { return b < hi ? (int)((hi - b) < 64 ? (hi - b) : 64) : 0; };
+            ReadFields F = load_fields(A, lo, chunk_nr(lo), lane);
             for (int64_t base = lo; base < hi; base += 64) {
-                const int nr = (int)((hi - base) < 64 ? (hi - base) : 64);
-                process_chunk<QUAL, K>(A, base, nr, lane, s8, gb, t0, P, edge, beyond, bmask, myrec, mystage,
-                                       qual_vec, W, it4, cnt, acc, pending, bad);
+                process_chunk<QUAL, K>(A, base, chunk_nr(base), F, base + 64, chunk_nr(base + 64), lane, s8, gb, t0, P,
+                                       edge, beyond, bmask, myrec, mystage, qual_vec, W, it4, cnt, acc, pending, bad);
                 __builtin_amdgcn_wave_barrier();
             }
             flush_acc(acc, cnt);
@@ -759,7 +831,7 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         static bool attr_set = false;                                                                        \
         if (!attr_set) {                                                                                     \
             (void)hipFuncSetAttribute((const void*)k_pileup<Q, KK, ST>,                                      \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);               \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);        \
             attr_set = true;                                                                                 \
         }                                                                                                    \
         hipLaunchKernelGGL((k_pileup<Q, KK, ST>), grid, block, lds, s, A);                                   \

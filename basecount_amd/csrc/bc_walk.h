@@ -155,6 +155,26 @@ __device__ __forceinline__ uint32_t qual_nibmask(uint32_t q0, uint32_t q1, uint3
     return __builtin_amdgcn_perm(b1, b0, 0x06040200u);
 }
 
+// ---- LDS-DMA staging (global_load_lds_dwordx4): bytes [src, src + bytes) -> LDS [dst, ...) -----
+// One wave-instruction moves 1 KiB lane-linearly (dst + 16 * lane), with no VGPR destination, so
+// all passes of a chunk's copy are in flight together (a register copy waits for every load
+// before its LDS write: one full memory round trip per KiB).  `dst` and `src` are 16-B aligned;
+// the source buffer is readable up to the next 16-B boundary.  `tid` / `nthreads`: the copying
+// threads (a wave: lane / 64; a block: threadIdx.x / blockDim.x).  hipcc does not count these
+// loads: the caller waits with stage_wait() before anything reads the stage.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+template <int NTHREADS>
+__device__ __forceinline__ void stage_dma(uint8_t* dst, const uint8_t* src, uint32_t bytes, int tid) {
+    const uint32_t wave_base = (uint32_t)(tid & ~63) * 16u;
+    for (uint32_t off = wave_base; off < bytes; off += NTHREADS * 16u) {  // wave-uniform
+        const uint32_t mine = off + (uint32_t)(tid & 63) * 16u;
+        if (mine < bytes)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + mine), (lds_void_t*)(dst + off), 16, 0, 0);
+    }
+}
+__device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // The 8 event classes at nibble indices n0 .. n0+7 of the sequence (unstaged: global memory).
 
 // Where a walk reads its event classes: the chunk's stage in LDS (nibble indices relative to the

@@ -290,14 +290,33 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
                           h->qual ? (size_t)h->qual_bytes : 0};
     const size_t cp[7] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6]};
     const void* src[7] = {h->pos, h->cig_beg, h->cig_n, h->seq_nib, h->cigar, h->seq, h->qual};
+    // ONE slab for the whole batch (arrays 4 KiB-aligned inside it, the slab a multiple of 2 MiB):
+    // the kernels' first touches of a batch then miss the GPU TLB on a few large fragments
+    // instead of on every small buffer's pages.  The first array present is the slab base
+    // (bc_reads_free).
+    size_t off[7], total = 0;
+    for (int i = 0; i < 7; ++i) {
+        off[i] = total;
+        total += (sz[i] + 4095) / 4096 * 4096;
+    }
+    total = (total + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+    if (std::getenv("BC_SLAB_PAD")) {  // diagnostic: arrays 2 MiB apart
+        total = 0;
+        for (int i = 0; i < 7; ++i) {
+            off[i] = total;
+            total += (sz[i] + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+        }
+    }
+    void* slab = nullptr;
+    HIP_TRY(hipMalloc(&slab, total));
     for (int i = 0; i < 7; ++i) {
         if (!sz[i]) continue;
-        hipError_t e = hipMalloc(&p[i], sz[i]);
-        if (e == hipSuccess && cp[i]) e = hipMemcpyAsync(p[i], src[i], cp[i], hipMemcpyHostToDevice, c->stream);
+        p[i] = (uint8_t*)slab + off[i];
+        hipError_t e = cp[i] ? hipMemcpyAsync(p[i], src[i], cp[i], hipMemcpyHostToDevice, c->stream) : hipSuccess;
         if (e == hipSuccess && i == 5) e = bc::launch_seq_event(c->stream, (const uint8_t*)p[5], h->seq_bytes, (uint8_t*)p[5]);
         if (e != hipSuccess) {
-            for (int j = 0; j <= i; ++j)
-                if (p[j]) (void)hipFree(p[j]);
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipFree(slab);
             return hip_fail(e, "bc_reads_upload");
         }
     }
@@ -318,8 +337,11 @@ int bc_reads_free(bc_ctx* c, bc_reads* d) {
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
     const void* p[7] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual};
-    for (auto q : p)
-        if (q) (void)hipFree((void*)q);
+    for (auto q : p)  // the first array present is the base of the batch's slab (bc_reads_upload)
+        if (q) {
+            (void)hipFree((void*)q);
+            break;
+        }
     std::memset(d, 0, sizeof *d);
     return BC_OK;
 }

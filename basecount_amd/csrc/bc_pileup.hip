@@ -17,6 +17,7 @@
 // Positions >= L (the last, partial tile and "edge" tiles past the reference end, up to the
 // furthest read end) do not count: a counted event there is the reference's std::out_of_range
 // (count.cpp:60-65,85) and is recorded as the first offending read index.
+#include <cstdio>
 #include <cstring>
 
 #include "bc_internal.h"
@@ -60,7 +61,23 @@ struct PileArgs {
     int64_t tiles_per_wave;  // k_pileup_solo: consecutive tiles swept by one wave
     int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 4 no walk, 8 no stats
                  // math, 16 no stores, 32 no sequence staging
+    unsigned long long* trace;  // diagnostic only (BC_TRACE): per-wave phase stamps, else null
 };
+
+// Diagnostic phase stamps (BC_TRACE builds the buffer; null otherwise): s_memrealtime (100 MHz,
+// chip-wide) of phase `ph` of this wave, written by lane 0 with a vector store.
+constexpr int kTracePhases = 12;
+// Compiled in only with -DBC_PHASE_TRACE (scripts/trace_phases.py): the stamps cost registers.
+__device__ __forceinline__ void trace_stamp(const PileArgs& A, int ph) {
+#ifdef BC_PHASE_TRACE
+    if (A.trace && (threadIdx.x & 63) == 0)
+        A.trace[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kTracePhases + ph] =
+            __builtin_amdgcn_s_memrealtime();
+#else
+    (void)A;
+    (void)ph;
+#endif
+}
 
 // Packed event of a "complex" read (more than 8 CIGAR ops, more than 4 runs, or huge indels)
 // at event index j (lane position - start): nibble index of the aligned base, kDel for a deletion
@@ -460,6 +477,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     __shared__ int64_t rng[8][2];  // per group: the tile's read range
     if (A.ablate & 64) return;
+    trace_stamp(A, 0);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nw = blockDim.x >> 6;
@@ -492,11 +510,27 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
         // the tile's reads [lo, hi): searched by the group's first wave (the S waves would all
         // find the same range), handed to the others through LDS
         int64_t lo = 0, hi = 0;
-        if (ws == 0 && t < A.n_tiles && !(A.ablate & 2))
+        if (ws == 0 && t < A.n_tiles && !(A.ablate & 2)) {
+#ifdef BC_PHASE_TRACE
+            if (A.trace) {  // diagnostic: latency of one dependent global load from here
+                const int32_t probe = A.pos[(lane * 1543) % (int)A.n];
+                if (probe == 0x7FFFFFFF) A.trace[0] = 1;
+                trace_stamp(A, 8);
+                const int32_t probe2 = A.pos[(lane * 977 + 5 + (probe & 1)) % (int)A.n];
+                if (probe2 == 0x7FFFFFFF) A.trace[0] = 1;
+                trace_stamp(A, 10);
+                const int32_t probe3 = A.cigar[(lane * 977 + 11 + (probe2 & 1)) % (int)A.n];
+                if (probe3 == 0x7FFFFFFF) A.trace[0] = 1;
+                trace_stamp(A, 11);
+            }
+#endif
             lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
+            trace_stamp(A, 9);
+        }
         if (S > 1) {
             if (ws == 0 && lane == 0) rng[g][0] = lo, rng[g][1] = hi;
             __syncthreads();
+            trace_stamp(A, 1);
             lo = rng[g][0];
             hi = rng[g][1];
         }
@@ -521,11 +555,18 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             auto chunk_nr = [&](int64_t b) { return b < hi ? (int)((hi - b) < 64 ? (hi - b) : 64) : 0; };
             int64_t base = lo + (int64_t)ws * 64;
             ReadFields F = load_fields(A, base, chunk_nr(base), lane);
+#ifdef BC_PHASE_TRACE
+            int nch = 0;
+#endif
             for (; base < hi; base += (int64_t)S * 64) {
                 const int64_t nb = base + (int64_t)S * 64;
                 process_chunk<QUAL, K>(A, base, chunk_nr(base), F, nb, chunk_nr(nb), lane, s8, gb, t0, P, edge,
                                        beyond, bmask, myrec, mystage, qual_vec, W, it4, cnt, acc, pending, bad);
                 __builtin_amdgcn_wave_barrier();
+#ifdef BC_PHASE_TRACE
+                if (nch < 2) trace_stamp(A, 2 + nch);
+                ++nch;
+#endif
             }
             flush_acc(acc, cnt);
             if (it4) swar_fold<K>(W, cnt, s8);
@@ -542,6 +583,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
 #pragma unroll
             for (int c = 0; c < K; ++c) red_of(wave)[c * kTile + lane] = cnt[c];
             __syncthreads();
+            trace_stamp(A, 4);
             if (ws == 0)
                 for (int w2 = wave + 1; w2 < wave + S; ++w2) {
 #pragma unroll
@@ -565,9 +607,11 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             continue;
         }
         __syncthreads();
+        trace_stamp(A, 5);
         // ---- fused kernel 2: per-lane fp64 terms, then ordered sums per position
         if (own) tile_terms<K>(A, &fin[g][0][0], terms_g, t0, ws * 64 + lane, S * 64);
         __syncthreads();
+        trace_stamp(A, 6);
         if (own && ws == 0 && P < L) {
             int64_t cov = 0;
             uint32_t mx = 0;
@@ -598,6 +642,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             A.sec[P] = h2;
         }
         __syncthreads();
+        trace_stamp(A, 7);
     }
 }
 
@@ -825,6 +870,19 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
     blocks = (blocks + 7) / 8 * 8;  // a multiple of the XCD count (see the kernel's tile mapping)
     const dim3 grid((unsigned)blocks), block(64 * nw);
     const size_t lds = pileup_lds_bytes(nw, groups);
+    // diagnostic only: BC_TRACE=<file> dumps the per-wave phase stamps of the 20th launch
+    static unsigned long long* tbuf = nullptr;
+    static int tcalls = 0;
+#ifdef BC_PHASE_TRACE
+    const char* tpath = std::getenv("BC_TRACE");
+#else
+    const char* tpath = nullptr;
+#endif
+    const size_t tn = (size_t)blocks * nw * kTracePhases;
+    if (tpath) {
+        if (!tbuf && hipMallocManaged((void**)&tbuf, 8 * (size_t)256 * 64 * 16 * kTracePhases) != hipSuccess) tbuf = nullptr;
+        if (tn <= (size_t)256 * 64 * 16 * kTracePhases) A.trace = tbuf;
+    }
     // > 64 KiB of dynamic LDS must be allowed per kernel (160 KiB per CU on gfx950)
 #define BC_PILE(Q, KK, ST)                                                                                   \
     do {                                                                                                     \
@@ -835,6 +893,13 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
             attr_set = true;                                                                                 \
         }                                                                                                    \
         hipLaunchKernelGGL((k_pileup<Q, KK, ST>), grid, block, lds, s, A);                                   \
+        if (A.trace && ++tcalls == 20) {                                                                     \
+            (void)hipStreamSynchronize(s);                                                                   \
+            if (FILE* f = std::fopen(tpath, "wb")) {                                                         \
+                std::fwrite(A.trace, 8, tn, f);                                                              \
+                std::fclose(f);                                                                              \
+            }                                                                                                \
+        }                                                                                                    \
     } while (0)
     if (mbq > 0) {
         if (k == 5) {

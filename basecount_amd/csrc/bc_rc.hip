@@ -27,15 +27,23 @@
 namespace bc {
 namespace {
 
-constexpr int kRcThreads = 256;
-constexpr int kRcReads = 256;   // reads per chunk (one per thread at setup)
-constexpr int kStage = 19968;   // staged sequence bytes per chunk (256 reads x 150 bp fit)
+// Chunk geometry: NT threads = NT reads per chunk (one per thread at setup), 78 staged sequence
+// bytes per read (150 bp reads fit with room).  Bigger chunks amortize the per-chunk setup
+// (barriers, reductions, window tables, flush atomics) and give every window more 64-read
+// slices, so a wave folds its counters less often.
+template <int NT>
+struct RcGeo {
+    static constexpr int kThreads = NT;
+    static constexpr int kReads = NT;
+    static constexpr int kStage = 78 * NT;
+    static constexpr int kWaves = NT / 64;
+};
+constexpr int kRcChunk = 256;  // default reads per chunk (BC_RC_CHUNK=256|512|1024 overrides)
 constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's first base
 #include "bc_walk.h"
 
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
 constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
-constexpr int kRcWaves = kRcThreads / 64;
 
 struct RcArgs {
     const int32_t* pos;
@@ -59,7 +67,7 @@ struct RcArgs {
 
 // Block-wide reduction of 8 values (max or min per slot): wave reduce, then LDS across waves.
 // Must be called by the whole block.
-template <int NV>
+template <int NV, int NWAVES>
 __device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -71,7 +79,7 @@ __device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         uint32_t r = red[0][k];
-        for (int w = 1; w < kRcWaves; ++w) {
+        for (int w = 1; w < NWAVES; ++w) {
             const uint32_t o = red[w][k];
             r = is_max[k] ? (o > r ? o : r) : (o < r ? o : r);
         }
@@ -134,9 +142,11 @@ __device__ void rc_complex(const RcArgs& A, int64_t r, int64_t& bad) {
     }
 }
 
-template <bool QUAL, int NC>
-__global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
-    __shared__ uint4 rec[kRcReads * 3];                                  // 12 KB
+template <bool QUAL, int NC, int NT>
+__global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
+    using Geo = RcGeo<NT>;
+    constexpr int kRcThreads = Geo::kThreads, kRcReads = Geo::kReads, kStage = Geo::kStage, kRcWaves = Geo::kWaves;
+    __shared__ uint4 rec[kRcReads * 3];                                  // 48 B per read
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 32];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
     __shared__ uint32_t red[kRcWaves][8];
@@ -186,9 +196,7 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
         const uint32_t buf_end = (uint32_t)(A.seq_words * 4 < 0xFFFFFFFFll ? A.seq_words * 4 : 0xFFFFFFFFll);
         spec_hi = spec_hi < buf_end ? spec_hi : buf_end;
         const bool spec = !QUAL && spec_hi > spec_lo && spec_hi - spec_lo <= (uint32_t)kStage && !(A.ablate & 512);
-        if (spec)
-            for (uint32_t off = tid * 16u; off < spec_hi - spec_lo; off += kRcThreads * 16u)
-                *(uint4*)(stage + off) = *(const uint4*)(A.seq + spec_lo + off);
+        if (spec) stage_dma<kRcThreads>(stage, A.seq + spec_lo, spec_hi - spec_lo, tid);
         RunTable T;
         T.nrun = 0;
         T.gap = T.complex = false;
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
                          simple ? (uint32_t)T.nrun : 0u,
                          (simple && T.gap) ? 1u : 0u};
         const bool is_max[7] = {false, true, false, true, true, true, true};
-        block_reduce<7>(v, is_max, red);  // contains a __syncthreads
+        block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
         const int64_t P0 = v[0], P1 = v[1];
         uint32_t seg_lo = v[2];
         const uint32_t seg_hi = v[3];
@@ -238,9 +246,13 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
         const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
         if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
         const bool staged = spec_ok || seg_hi - seg_lo <= (uint32_t)kStage;
-        if (spec && !spec_ok) __syncthreads();  // (uniform) the speculative copy is overwritten
+        if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
+            stage_wait();
+            __syncthreads();
+        }
         // ---- stage the chunk's sequence exactly (16 B per thread per pass) unless done above
-        if (staged && !spec_ok && !(A.ablate & 512)) {
+        if (!QUAL && staged && !spec_ok && !(A.ablate & 512)) stage_dma<kRcThreads>(stage, A.seq + seg_lo, seg_hi - seg_lo, tid);
+        if (QUAL && staged && !spec_ok && !(A.ablate & 512)) {
             for (uint32_t off = tid * 16u; off < seg_hi - seg_lo; off += kRcThreads * 16u) {
                 uint4 q4 = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
                 if (QUAL) {
@@ -280,6 +292,7 @@ __global__ __launch_bounds__(kRcThreads) void k_rc(RcArgs A) {
             rec[tid * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
             rec[tid * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
         }
+        if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
         __syncthreads();  // stage, records and the complex-read list complete
         fetch_fields(chunk + gridDim.x);  // in flight during the walk
         const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
@@ -448,20 +461,34 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     A.mbq = mbq;
     A.seq_words = (int64_t)(seq_event_bytes(r.seq_bytes) / 4);
     A.qual_bytes = r.qual ? r.qual_bytes : 0;
-    A.n_chunks = (r.n_reads + kRcReads - 1) / kRcReads;
     A.counts = counts;
     A.err = d_err;
     A.ablate = 0;
     if (const char* ab = std::getenv("BC_ABLATE")) A.ablate = std::atoi(ab);
-    int64_t blocks = A.n_chunks < 256 * 4 ? A.n_chunks : 256 * 4;
-    const dim3 grid((unsigned)blocks), block(kRcThreads);
+    int nt = kRcChunk;
+    if (const char* e = std::getenv("BC_RC_CHUNK")) nt = std::atoi(e);
+    nt = nt >= 1024 ? 1024 : (nt >= 512 ? 512 : 256);
+    A.n_chunks = (r.n_reads + nt - 1) / nt;
+    // resident blocks: 1024 threads' worth of LDS-bound blocks per CU
+    const int64_t cap = 256 * (1024 / nt);
+    const int64_t blocks = A.n_chunks < cap ? A.n_chunks : cap;
+    const dim3 grid((unsigned)blocks), block(nt);
+#define BC_RC(Q, KK, NTT) hipLaunchKernelGGL((k_rc<Q, KK, NTT>), grid, block, 0, s, A)
+#define BC_RC_NT(Q, KK)                                 \
+    do {                                                \
+        if (nt == 1024) BC_RC(Q, KK, 1024);             \
+        else if (nt == 512) BC_RC(Q, KK, 512);          \
+        else BC_RC(Q, KK, 256);                         \
+    } while (0)
     if (mbq > 0) {
-        if (ncols == 6) hipLaunchKernelGGL((k_rc<true, 6>), grid, block, 0, s, A);
-        else hipLaunchKernelGGL((k_rc<true, 5>), grid, block, 0, s, A);
+        if (ncols == 6) BC_RC_NT(true, 6);
+        else BC_RC_NT(true, 5);
     } else {
-        if (ncols == 6) hipLaunchKernelGGL((k_rc<false, 6>), grid, block, 0, s, A);
-        else hipLaunchKernelGGL((k_rc<false, 5>), grid, block, 0, s, A);
+        if (ncols == 6) BC_RC_NT(false, 6);
+        else BC_RC_NT(false, 5);
     }
+#undef BC_RC_NT
+#undef BC_RC
     return hipGetLastError();
 }
 

@@ -7,7 +7,11 @@ all-M CIGAR).  At N>1 every rank runs its own contig of that shape (contig shard
 scaling, no collective inside the step); the per-contig results are gathered to rank 0 over
 RCCL once after the timed region (reported as gather_ms).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5] [--launch graph|eager]
+
+The K timed steps are captured into one hipGraph and launched once (default; --launch eager
+issues them one by one): the same kernels on the same data, without the per-launch host and
+command-processor gaps that a ~15 us step otherwise pays.
 
 C5 (24 human-chromosome-sized contigs, 3.09 Gb, 1.2 M reads) is summary-shaped: the per-position
 percentages are not stored (main.py's --summarise never prints them).
@@ -107,6 +111,8 @@ def main():
     ap.add_argument("--mbq", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
+                    help="graph: the K timed steps are captured into ONE hipGraph and launched once")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,12 +197,20 @@ def main():
     # ---- timed region: K eager back-to-back steps, bracketed by barrier + device sync; hipEvents
     # on the library's stream (the stream every launch goes to) around the region give the
     # on-device time per step ---------------------------------------------------------------
+    graph = None
+    if args.launch == "graph":  # the same K steps, replayed from one captured graph
+        graph = ctx.capture(lambda: [step() for _ in range(args.steps)])
+        graph.launch()  # untimed replay (first-launch setup)
+        ctx.sync()
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
     ctx.event_record(0)
-    for _ in range(args.steps):
-        step()
+    if graph is not None:
+        graph.launch()
+    else:
+        for _ in range(args.steps):
+            step()
     ctx.event_record(1)
     ctx.sync()
     barrier()
@@ -323,7 +337,7 @@ def main():
             "kernel_us": {kernel_names[n]: v * 1e6 for n, v in kern_s.items()},
             "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per contig per step"
                         if dom == "pileup" else "memset + k_rc (kernel 1) + k_stats (kernel 2) per contig per step")
-                       + ", eager launches",
+                       + (", the K timed steps replayed from one hipGraph" if graph is not None else ", eager launches"),
             "parity_vs_oracle": parity,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

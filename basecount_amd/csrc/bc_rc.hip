@@ -370,34 +370,46 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
                     ghi = U(whi[g]);
                 }
                 const int gb = (int)(PB + 8 * g);
+                // two items of the same window per step when there are (two independent LDS
+                // chains in flight); the step's reads r and r + 64
+                const bool two = k + 1 < k1w && k + 1 < gnext;  // (uniform)
                 const uint32_t r = glo + 64u * (k - gpre) + (uint32_t)lane;
-                const bool in = r < ghi;
-                const int rs = in ? (int)r : 0;
-                uint32_t x;
-                if (A.ablate & 256) {
-                    x = rec[rs * 3].x * 0x01010101u;
-                } else if (maxrun <= 1) {
-                    x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
-                                      : window_events<1, true, false, QUAL>(src, rec, rs, gb))
-                            : (staged ? window_events<1, false, true, QUAL>(src, rec, rs, gb)
-                                      : window_events<1, false, false, QUAL>(src, rec, rs, gb));
-                } else if (maxrun == 2) {
-                    x = staged ? window_events<2, true, true, QUAL>(src, rec, rs, gb)
-                               : window_events<2, true, false, QUAL>(src, rec, rs, gb);
-                } else {
-                    x = staged ? window_events<4, true, true, QUAL>(src, rec, rs, gb)
-                               : window_events<4, true, false, QUAL>(src, rec, rs, gb);
-                }
-                x = in ? x : 0u;
+                auto events = [&](uint32_t rr) {
+                    const int rs = rr < ghi ? (int)rr : 0;
+                    uint32_t x;
+                    if (A.ablate & 256) {
+                        x = rec[rs * 3].x * 0x01010101u;
+                    } else if (maxrun <= 1) {
+                        x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
+                                          : window_events<1, true, false, QUAL>(src, rec, rs, gb))
+                                : (staged ? window_events<1, false, true, QUAL>(src, rec, rs, gb)
+                                          : window_events<1, false, false, QUAL>(src, rec, rs, gb));
+                    } else if (maxrun == 2) {
+                        x = staged ? window_events<2, true, true, QUAL>(src, rec, rs, gb)
+                                   : window_events<2, true, false, QUAL>(src, rec, rs, gb);
+                    } else {
+                        x = staged ? window_events<4, true, true, QUAL>(src, rec, rs, gb)
+                                   : window_events<4, true, false, QUAL>(src, rec, rs, gb);
+                    }
+                    return rr < ghi ? x : 0u;
+                };
+                uint32_t x0 = events(r), x1 = two ? events(r + 64u) : 0u;
                 if ((int64_t)gb + 8 > A.L) {  // window reaches past the reference end
                     int64_t kL = A.L - gb;
                     kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
                     const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
-                    if ((x & bmask) && c0 + (int64_t)r < bad) bad = c0 + (int64_t)r;
-                    x &= ~bmask;
+                    if ((x0 & bmask) && c0 + (int64_t)r < bad) bad = c0 + (int64_t)r;
+                    if ((x1 & bmask) && c0 + (int64_t)r + 64 < bad) bad = c0 + (int64_t)r + 64;
+                    x0 &= ~bmask;
+                    x1 &= ~bmask;
                 }
-                swar_add<NC>(W, x);
-                if (++it4 == 14) {
+                swar_add<NC>(W, x0);
+                if (two) {
+                    swar_add<NC>(W, x1);
+                    ++k;
+                    ++it4;
+                }
+                if (++it4 >= 13) {  // every nibble counter <= 14
                     rc_fold<NC>(W, hist, g, s8, A.ablate);
                     it4 = 0;
                 }

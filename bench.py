@@ -239,7 +239,9 @@ def main():
     # alone (a one-kernel step: the step region itself)
     kern_s = {}
     if launched == ["pileup"]:
-        kern_s["pileup"] = dev_step
+        # eager launches: the kernel's own average duration (what rocprofv3's kernel trace
+        # reports); a graph replay hides part of the launch gap and would flatter the roofline
+        kern_s["pileup"] = dev_step if graph is None else region(step, max(3, min(args.steps, 100)))
     else:  # deep batches: memset + k_rc + k_stats (bc_count on the same batch launches k_rc alone)
         reps = max(3, min(args.steps, 50))
 

@@ -20,6 +20,7 @@
 // atomics.  Counted events at positions >= L are the reference's std::out_of_range
 // (count.cpp:60-65,85): the first offending read index is kept (atomicMin), nothing is counted
 // there.  Kernel 2 (k_stats) runs afterwards on the counts.
+#include <cstdio>
 #include <cstring>
 
 #include "bc_internal.h"
@@ -38,12 +39,29 @@ struct RcGeo {
     static constexpr int kStage = 78 * NT;
     static constexpr int kWaves = NT / 64;
 };
-constexpr int kRcChunk = 256;  // default reads per chunk (BC_RC_CHUNK=256|512|1024 overrides)
+constexpr int kRcChunk = 256;
+constexpr int kImgRows = 24;  // windows an imaged chunk may cover (event image rows)
 constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's first base
 #include "bc_walk.h"
 
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
 constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
+
+// Diagnostic phase totals (-DBC_PHASE_TRACE): per wave, cycles spent in each chunk phase,
+// summed over its chunks (s_memtime), written once at the end.  Costs registers.
+#ifdef BC_PHASE_TRACE
+#define RC_STAMP(ph)                                                                 \
+    do {                                                                             \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();                          \
+        if ((ph) > 0) tsum[(ph) - 1] += now_ - tlast;                                \
+        tlast = now_;                                                                \
+    } while (0)
+#else
+#define RC_STAMP(ph) \
+    do {             \
+    } while (0)
+#endif
+constexpr int kRcPhases = 7;
 
 struct RcArgs {
     const int32_t* pos;
@@ -62,7 +80,8 @@ struct RcArgs {
     int32_t* counts;  // [ncols][L], accumulated into
     unsigned long long* err;
     int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events,
-                 // 512 no staging, 2048 no flush
+                 // 512 no staging, 2048 no flush, 8192 no event image
+    unsigned long long* trace;  // diagnostic only (BC_PHASE_TRACE builds): [block][wave][kRcPhases]
 };
 
 // Block-wide reduction of 8 values (max or min per slot): wave reduce, then LDS across waves.
@@ -143,10 +162,15 @@ __device__ void rc_complex(const RcArgs& A, int64_t r, int64_t& bad) {
 }
 
 template <bool QUAL, int NC, int NT>
-__global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
+__global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     using Geo = RcGeo<NT>;
     constexpr int kRcThreads = Geo::kThreads, kRcReads = Geo::kReads, kStage = Geo::kStage, kRcWaves = Geo::kWaves;
-    __shared__ uint4 rec[kRcReads * 3];                                  // 48 B per read
+    // records (48 B per read) of the run-table walk, or, on the image path, the chunk's event
+    // image: kImgRows window rows x kRcReads reads of BC_SEQ_EVENT words
+    constexpr int kRecU4 = kRcReads * 3, kImgU4 = kImgRows * kRcReads / 4;
+    __shared__ uint4 rec[kRecU4 > kImgU4 ? kRecU4 : kImgU4];
+    uint32_t* img = (uint32_t*)rec;
+    __shared__ int32_t rpos[kRcReads];  // the chunk's read positions (window tables)
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 32];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
     __shared__ uint32_t red[kRcWaves][8];
@@ -176,7 +200,11 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
     };
     fetch_fields(blockIdx.x);
 
+#ifdef BC_PHASE_TRACE
+    uint64_t tsum[kRcPhases] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+#endif
     for (int64_t chunk = blockIdx.x; chunk < A.n_chunks; chunk += gridDim.x) {
+        RC_STAMP(0);
         const int64_t c0 = chunk * kRcReads;
         const int nr = (int)(A.n - c0 < kRcReads ? A.n - c0 : kRcReads);
         // ---- 1. setup: one read per thread
@@ -235,7 +263,9 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
                          simple ? (uint32_t)T.nrun : 0u,
                          (simple && T.gap) ? 1u : 0u};
         const bool is_max[7] = {false, true, false, true, true, true, true};
+        RC_STAMP(1);
         block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
+        RC_STAMP(2);
         const int64_t P0 = v[0], P1 = v[1];
         uint32_t seg_lo = v[2];
         const uint32_t seg_hi = v[3];
@@ -246,6 +276,12 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
         const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
         if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
         const bool staged = spec_ok || seg_hi - seg_lo <= (uint32_t)kStage;
+        // event-image path: a staged chunk of reads with <= 2 runs whose windows fit the image.
+        // Each read's events are extracted ONCE per window (lane = read, its windows in a row)
+        // instead of once per (window, run) item from the run table.
+        const int64_t WBc = P0 & ~(int64_t)7;
+        const int NWc = (int)(P1 > WBc ? (P1 - WBc + 7) / 8 : 0);
+        const bool img_path = staged && maxrun <= 2 && NWc <= kImgRows && !(A.ablate & 8192);
         if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
             stage_wait();
             __syncthreads();
@@ -288,19 +324,155 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
                 rr[k] = simple ? pack_rr(T.st[k], T.en[k]) : 0u;
                 nb[k] = msn - qbase + (uint32_t)T.qd[k];
             }
-            rec[tid * 3] = make_uint4(mpos, simple ? T.span * 4u : 0u, rr[0], nb[0]);
-            rec[tid * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
-            rec[tid * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
+            if (!img_path) {
+                rec[tid * 3] = make_uint4(mpos, simple ? T.span * 4u : 0u, rr[0], nb[0]);
+                rec[tid * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
+                rec[tid * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
+            }
+            rpos[tid] = (int32_t)mpos;
         }
         if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
         __syncthreads();  // stage, records and the complex-read list complete
+        RC_STAMP(3);
+        if (img_path) {
+            // ---- event image: thread tid writes column tid, rows = the chunk's windows
+            // [G0, G0 + NWc): the 8 event classes its read has in each (zero outside the read)
+            const int p7 = (int)(mpos & 7u);
+            const int G0 = (int)(U((uint32_t)P0) >> 3);
+            const int i0 = (int)(mpos >> 3) - G0;  // the read's first window row
+            const int nwr = simple ? (p7 + (int)T.span + 7) >> 3 : 0;
+            const int qb = (int)(staged ? 2u * seg_lo : 0u);
+            // run k: stage nibble of stream position 0 (= window row i0, nibble 0)
+            const int s0 = (int)msn - qb + T.qd[0] - p7, s1 = (int)msn - qb + T.qd[1] - p7;
+            const int wb0 = s0 >> 3, wb1 = s1 >> 3;
+            const uint32_t sh0 = (uint32_t)(s0 & 7) * 4u, sh1 = (uint32_t)(s1 & 7) * 4u;
+            // thresholds in stream bits (4 per nibble): runs [A_k, B_k), read [Z, SP)
+            const int Z = 4 * p7, SP = 4 * (p7 + (int)T.span);
+            const int A0 = 4 * (p7 + (int)T.st[0]), B0 = 4 * (p7 + (int)T.en[0]);
+            const int A1 = 4 * (p7 + (int)T.st[1]), B1 = 4 * (p7 + (int)T.en[1]);
+            const uint32_t* sw = (const uint32_t*)stage;
+            auto thr = [](int c) {  // bits below clamp(c, 0, 32)
+                c = c < 0 ? 0 : (c > 32 ? 32 : c);
+                return (uint32_t)(1ull << c) - 1u;
+            };
+            for (int row = 0; row < NWc; ++row) {  // NWc uniform
+                const int i = row - i0;
+                uint32_t x = 0u;
+                if (i >= 0 && i < nwr) {
+                    const int c = 32 * i;
+                    const uint32_t v0 = __builtin_amdgcn_alignbit(sw[wb0 + i + 1], sw[wb0 + i], sh0);
+                    const uint32_t t0 = thr(A0 - c), t1 = thr(B0 - c);
+                    x = v0 & t1 & ~t0;
+                    uint32_t runs = t1 & ~t0;
+                    if (maxrun == 2) {  // (uniform)
+                        const uint32_t v1 = __builtin_amdgcn_alignbit(sw[wb1 + i + 1], sw[wb1 + i], sh1);
+                        const uint32_t t2 = thr(A1 - c), t3 = thr(B1 - c);
+                        x |= v1 & t3 & ~t2;
+                        runs |= t3 & ~t2;
+                    }
+                    if (gap) x |= kClsDel & thr(SP - c) & ~thr(Z - c) & ~runs;
+                }
+                const int64_t rb = 8 * (int64_t)(G0 + row);  // (uniform) the row's first position
+                if (rb + 8 > A.L) {  // events at positions >= L: the reference's out_of_range
+                    int64_t kL = A.L - rb;
+                    kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
+                    const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
+                    if ((x & bmask) && c0 + tid < bad) bad = c0 + tid;
+                    x &= ~bmask;
+                }
+                img[row * kRcReads + tid] = x;
+            }
+        }
         fetch_fields(chunk + gridDim.x);  // in flight during the walk
         const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
                          staged ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
         const int64_t WB = P0 & ~(int64_t)7;
+        const int G0w = (int)(WB >> 3);  // the image's first window (image path)
         const int64_t NW = P1 > WB ? (P1 - WB + 7) / 8 : 0;
-        // ---- 2./3. window passes of up to kRcWin windows
-        for (int64_t wp = 0; wp < NW; wp += kRcWin) {
+        if (img_path) {
+            __syncthreads();  // the image complete (columns are written by their read's thread)
+            RC_STAMP(4);
+            // ---- image path, transposed: thread (row g = tid & 31, read group q = tid >> 5) adds
+            // the 32 reads [32q, 32q + 32) of window row g into SWAR nibble counters (zero image
+            // words for reads outside the window), byte counters per class every <= 15 reads.
+            // Lanes g and g + 32 of a wave hold the same row (groups 2w, 2w + 1): summed with a
+            // lane swap; the 4 waves through LDS; thread g < 32 flushes its 8 positions.
+            uint32_t (*part)[2 * 6][32] = (uint32_t (*)[2 * 6][32])&hist[0][0];  // [wave][2 NC][32]
+            const int gr = tid & 31, q = tid >> 5;
+            uint32_t blo[6] = {0u, 0u, 0u, 0u, 0u, 0u}, bhi[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+            if (!(A.ablate & 4)) {
+                const uint32_t* col = img + (gr < NWc ? gr : 0) * kRcReads + 32 * q;
+                Swar W;
+#pragma unroll
+                for (int c = 0; c < 6; ++c) W.a4[c] = 0;
+                auto fold = [&]() {
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        blo[c] += W.a4[c] & 0x0F0F0F0Fu;
+                        bhi[c] += (W.a4[c] >> 4) & 0x0F0F0F0Fu;
+                        W.a4[c] = 0;
+                    }
+                };
+#pragma unroll
+                for (int rr = 0; rr < 32; ++rr) {
+                    swar_add<NC>(W, col[rr]);
+                    if (rr == 14 || rr == 29) fold();
+                }
+                fold();
+                if (gr >= NWc) {
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) blo[c] = bhi[c] = 0;
+                }
+            }
+            // bytes <= 64 after the lane swap (two groups of 32 reads)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                blo[c] += (uint32_t)__shfl_xor((int)blo[c], 32);
+                bhi[c] += (uint32_t)__shfl_xor((int)bhi[c], 32);
+            }
+            if (lane < 32) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    part[wave][2 * c][lane] = blo[c];
+                    part[wave][2 * c + 1][lane] = bhi[c];
+                }
+            }
+            __syncthreads();  // the waves' partial rows
+            RC_STAMP(5);
+            // the rows' final counts in LDS (the image is dead), [class][position]
+            uint32_t* fin = img;
+            if (tid < 32 && tid < NWc) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    // byte k of the lo (hi) word = position 2k (2k + 1); 4 waves x <= 64 fits 16 bits
+                    uint32_t e = 0, o = 0, e2 = 0, o2 = 0;
+#pragma unroll
+                    for (int w = 0; w < kRcWaves; ++w) {
+                        const uint32_t vl = part[w][2 * c][tid], vh = part[w][2 * c + 1][tid];
+                        e += vl & 0x00FF00FFu;         // positions 0, 4 (16-bit halves)
+                        e2 += (vl >> 8) & 0x00FF00FFu;  // positions 2, 6
+                        o += vh & 0x00FF00FFu;         // positions 1, 5
+                        o2 += (vh >> 8) & 0x00FF00FFu;  // positions 3, 7
+                    }
+                    uint32_t* f = fin + c * 8 * kImgRows + 8 * tid;
+                    f[0] = e & 0xFFFFu, f[1] = o & 0xFFFFu, f[2] = e2 & 0xFFFFu, f[3] = o2 & 0xFFFFu;
+                    f[4] = e >> 16, f[5] = o >> 16, f[6] = e2 >> 16, f[7] = o2 >> 16;
+                }
+            }
+            __syncthreads();  // the chunk's counts complete
+            // flush: one position per thread, 256 contiguous bytes per atomic wave-instruction
+            for (int t = tid; t < ((A.ablate & 2048) ? 0 : 8 * NWc); t += kRcThreads) {
+                const int64_t p = 8 * (int64_t)G0w + t;
+                if (p >= A.L) break;
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const uint32_t v = fin[c * 8 * kImgRows + t];
+                    if (v) atomicAdd(&A.counts[(int64_t)c * A.L + p], (int32_t)v);
+                }
+            }
+        }
+        // ---- 2./3. window passes of up to kRcWin windows (run-table walk)
+        for (int64_t wp = 0; wp < (img_path ? 0 : NW); wp += kRcWin) {
             const int nwin = (int)(NW - wp < kRcWin ? NW - wp : kRcWin);
             const int64_t PB = WB + 8 * wp;
             for (int t = tid; t < 3 * kRcWinPos; t += kRcThreads) (&hist[0][0])[t] = 0u;
@@ -312,8 +484,8 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
                     const int64_t w = p >= PB ? (p - PB) >> 3 : -1;
                     return (int)(w < 0 ? 0 : (w > nwin ? nwin : w));
                 };
-                const int64_t p_t = rec[tid * 3].x;
-                const int64_t p_n = tid + 1 < nr ? (int64_t)rec[(tid + 1) * 3].x : INT64_MAX / 2;
+                const int64_t p_t = rpos[tid];
+                const int64_t p_n = tid + 1 < nr ? (int64_t)rpos[tid + 1] : INT64_MAX / 2;
                 // hi: b_g = #{pos < gb + 8} = t + 1 for g in [win(p_t), win(p_next))
                 const int b0 = tid == 0 ? 0 : win_of(p_t), b1 = tid + 1 < nr ? win_of(p_n) : nwin;
                 if (tid == 0)
@@ -377,7 +549,9 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
                 auto events = [&](uint32_t rr) {
                     const int rs = rr < ghi ? (int)rr : 0;
                     uint32_t x;
-                    if (A.ablate & 256) {
+                    if (img_path) {
+                        x = img[(int)(gb / 8 - G0w) * kRcReads + rs];
+                    } else if (A.ablate & 256) {
                         x = rec[rs * 3].x * 0x01010101u;
                     } else if (maxrun <= 1) {
                         x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
@@ -434,7 +608,13 @@ __global__ __launch_bounds__(NT, 4) void k_rc(RcArgs A) {
         const uint32_t nc = U(ncx);
         for (uint32_t q = wave; q < nc; q += kRcWaves) rc_complex<QUAL, NC>(A, c0 + cxl[q], bad);
         __syncthreads();  // records / stage / cxl reused by the next chunk
+        RC_STAMP(6);
     }
+#ifdef BC_PHASE_TRACE
+    if (A.trace && lane == 0)
+        for (int k = 0; k < kRcPhases; ++k)
+            A.trace[((size_t)blockIdx.x * kRcWaves + wave) * kRcPhases + k] = tsum[k];
+#endif
     // first offending read of this block (std::out_of_range in the reference)
     for (int o = 32; o > 0; o >>= 1) {
         const int64_t b2 = __shfl_down(bad, o);
@@ -477,30 +657,40 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     A.err = d_err;
     A.ablate = 0;
     if (const char* ab = std::getenv("BC_ABLATE")) A.ablate = std::atoi(ab);
-    int nt = kRcChunk;
-    if (const char* e = std::getenv("BC_RC_CHUNK")) nt = std::atoi(e);
-    nt = nt >= 1024 ? 1024 : (nt >= 512 ? 512 : 256);
+    constexpr int nt = kRcChunk;
     A.n_chunks = (r.n_reads + nt - 1) / nt;
-    // resident blocks: 1024 threads' worth of LDS-bound blocks per CU
-    const int64_t cap = 256 * (1024 / nt);
+    // resident blocks: LDS bounds a CU to 3 (event image + stage + histogram)
+    const int64_t cap = 256 * 3;
     const int64_t blocks = A.n_chunks < cap ? A.n_chunks : cap;
     const dim3 grid((unsigned)blocks), block(nt);
-#define BC_RC(Q, KK, NTT) hipLaunchKernelGGL((k_rc<Q, KK, NTT>), grid, block, 0, s, A)
-#define BC_RC_NT(Q, KK)                                 \
-    do {                                                \
-        if (nt == 1024) BC_RC(Q, KK, 1024);             \
-        else if (nt == 512) BC_RC(Q, KK, 512);          \
-        else BC_RC(Q, KK, 256);                         \
-    } while (0)
+    A.trace = nullptr;
+#ifdef BC_PHASE_TRACE
+    // diagnostic only: BC_TRACE=<file> dumps the per-wave phase totals of the 20th launch
+    static unsigned long long* tbuf = nullptr;
+    static int tcalls = 0;
+    const char* tpath = std::getenv("BC_TRACE");
+    const size_t tn = (size_t)blocks * (nt / 64) * kRcPhases;
+    if (tpath && !tbuf) (void)hipMallocManaged((void**)&tbuf, tn * 8);
+    if (tpath) A.trace = tbuf;
+#endif
+#define BC_RC(Q, KK) hipLaunchKernelGGL((k_rc<Q, KK, nt>), grid, block, 0, s, A)
     if (mbq > 0) {
-        if (ncols == 6) BC_RC_NT(true, 6);
-        else BC_RC_NT(true, 5);
+        if (ncols == 6) BC_RC(true, 6);
+        else BC_RC(true, 5);
     } else {
-        if (ncols == 6) BC_RC_NT(false, 6);
-        else BC_RC_NT(false, 5);
+        if (ncols == 6) BC_RC(false, 6);
+        else BC_RC(false, 5);
     }
-#undef BC_RC_NT
 #undef BC_RC
+#ifdef BC_PHASE_TRACE
+    if (A.trace && ++tcalls == 20) {
+        (void)hipStreamSynchronize(s);
+        if (FILE* f = std::fopen(tpath, "wb")) {
+            std::fwrite(A.trace, 8, tn, f);
+            std::fclose(f);
+        }
+    }
+#endif
     return hipGetLastError();
 }
 

@@ -61,7 +61,7 @@ constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
     do {             \
     } while (0)
 #endif
-constexpr int kRcPhases = 7;
+[[maybe_unused]] constexpr int kRcPhases = 7;
 
 struct RcArgs {
     const int32_t* pos;
@@ -260,7 +260,13 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                          (simple && T.qlen) ? (msn >> 1) : 0xFFFFFFFFu,
                          (simple && T.qlen) ? ((msn + T.qlen + 1) >> 1) : 0u,
                          simple ? T.span : 0u,
-                         simple ? (uint32_t)T.nrun : 0u,
+                         // reads the event image cannot take (first run not at the read start, last
+                         // run not at its end) count as 3 runs: such a chunk takes the run tables
+                         simple ? ((T.nrun >= 1 && T.st[0] == 0u &&
+                                    (T.nrun == 1 ? T.en[0] : T.en[1]) == T.span) || T.nrun > 2
+                                       ? (uint32_t)T.nrun
+                                       : 3u)
+                                : 0u,
                          (simple && T.gap) ? 1u : 0u};
         const bool is_max[7] = {false, true, false, true, true, true, true};
         RC_STAMP(1);
@@ -340,47 +346,61 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const int p7 = (int)(mpos & 7u);
             const int G0 = (int)(U((uint32_t)P0) >> 3);
             const int i0 = (int)(mpos >> 3) - G0;  // the read's first window row
-            const int nwr = simple ? (p7 + (int)T.span + 7) >> 3 : 0;
             const int qb = (int)(staged ? 2u * seg_lo : 0u);
             // run k: stage nibble of stream position 0 (= window row i0, nibble 0)
             const int s0 = (int)msn - qb + T.qd[0] - p7, s1 = (int)msn - qb + T.qd[1] - p7;
             const int wb0 = s0 >> 3, wb1 = s1 >> 3;
             const uint32_t sh0 = (uint32_t)(s0 & 7) * 4u, sh1 = (uint32_t)(s1 & 7) * 4u;
-            // thresholds in stream bits (4 per nibble): runs [A_k, B_k), read [Z, SP)
-            const int Z = 4 * p7, SP = 4 * (p7 + (int)T.span);
-            const int A0 = 4 * (p7 + (int)T.st[0]), B0 = 4 * (p7 + (int)T.en[0]);
-            const int A1 = 4 * (p7 + (int)T.st[1]), B1 = 4 * (p7 + (int)T.en[1]);
+            // Stream bits (4 per nibble) from the image's first row: the read is [Z, SP), its
+            // first run [Z, B0), the deletions [B0, A1), the second run [A1, SP) (one-run reads:
+            // A1 = B0 = SP).  T(X) = bits of a row below X; row r's window is bits [32r, 32r + 32).
+            const int ob = 32 * i0 + 4 * p7;  // stream bit of the read's reference offset 0
+            const int Z = ob, SP = ob + 4 * (int)T.span;
+            const int B0 = ob + 4 * (int)T.en[0];
+            const int A1 = T.nrun == 2 ? ob + 4 * (int)T.st[1] : SP;
+            const int B0e = T.nrun == 2 ? B0 : SP;
+            const int lim = kStage / 4;
+            const int f0 = wb0 - i0, f1 = wb1 - i0;  // stage word of row r: f_k + r (clamped)
             const uint32_t* sw = (const uint32_t*)stage;
             auto thr = [](int c) {  // bits below clamp(c, 0, 32)
                 c = c < 0 ? 0 : (c > 32 ? 32 : c);
                 return (uint32_t)(1ull << c) - 1u;
             };
-            for (int row = 0; row < NWc; ++row) {  // NWc uniform
-                const int i = row - i0;
-                uint32_t x = 0u;
-                if (i >= 0 && i < nwr) {
-                    const int c = 32 * i;
-                    const uint32_t v0 = __builtin_amdgcn_alignbit(sw[wb0 + i + 1], sw[wb0 + i], sh0);
-                    const uint32_t t0 = thr(A0 - c), t1 = thr(B0 - c);
-                    x = v0 & t1 & ~t0;
-                    uint32_t runs = t1 & ~t0;
+            // stage word w (clamped into the stage and its pads); row r's 8 event classes of run k
+            // are the funnel shift of words f_k + r, f_k + r + 1: one new word per row and run
+            auto word = [&](int w) { return sw[w < -1 ? -1 : (w > lim ? lim : w)]; };
+            if (!simple) {
+#pragma unroll
+                for (int row = 0; row < kImgRows; ++row)
+                    if (row < NWc) img[row * kRcReads + tid] = 0u;
+            } else {
+                uint32_t p0 = word(f0), p1 = maxrun == 2 ? word(f1) : 0u;
+#pragma unroll
+                for (int row = 0; row < kImgRows; ++row) {
+                    if (row >= NWc) continue;  // (uniform)
+                    const int c = 32 * row;
+                    const uint32_t tz = thr(Z - c), tb = thr(B0e - c), ta = thr(A1 - c), ts = thr(SP - c);
+                    const uint32_t n0 = word(f0 + row + 1);
+                    const uint32_t v0 = __builtin_amdgcn_alignbit(n0, p0, sh0);
+                    p0 = n0;
+                    uint32_t x = v0 & tb & ~tz;
                     if (maxrun == 2) {  // (uniform)
-                        const uint32_t v1 = __builtin_amdgcn_alignbit(sw[wb1 + i + 1], sw[wb1 + i], sh1);
-                        const uint32_t t2 = thr(A1 - c), t3 = thr(B1 - c);
-                        x |= v1 & t3 & ~t2;
-                        runs |= t3 & ~t2;
+                        const uint32_t n1 = word(f1 + row + 1);
+                        const uint32_t v1 = __builtin_amdgcn_alignbit(n1, p1, sh1);
+                        p1 = n1;
+                        x |= v1 & ts & ~ta;
                     }
-                    if (gap) x |= kClsDel & thr(SP - c) & ~thr(Z - c) & ~runs;
+                    if (gap) x |= kClsDel & ta & ~tb;  // (uniform)
+                    const int64_t rb = 8 * (int64_t)(G0 + row);  // (uniform) the row's first position
+                    if (rb + 8 > A.L) {  // events at positions >= L: the reference's out_of_range
+                        int64_t kL = A.L - rb;
+                        kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
+                        const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
+                        if ((x & bmask) && c0 + tid < bad) bad = c0 + tid;
+                        x &= ~bmask;
+                    }
+                    img[row * kRcReads + tid] = x;
                 }
-                const int64_t rb = 8 * (int64_t)(G0 + row);  // (uniform) the row's first position
-                if (rb + 8 > A.L) {  // events at positions >= L: the reference's out_of_range
-                    int64_t kL = A.L - rb;
-                    kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
-                    const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
-                    if ((x & bmask) && c0 + tid < bad) bad = c0 + tid;
-                    x &= ~bmask;
-                }
-                img[row * kRcReads + tid] = x;
             }
         }
         fetch_fields(chunk + gridDim.x);  // in flight during the walk

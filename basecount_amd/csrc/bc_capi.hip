@@ -199,6 +199,7 @@ int bc_ctx_destroy(bc_ctx* c) {
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_err) (void)hipFree(c->d_err);
+    if (c->rc_scratch) (void)hipFree(c->rc_scratch);
     if (c->h_err) (void)hipHostFree(c->h_err);
     for (auto& v : c->ev)
         for (auto& pr : v) {
@@ -387,14 +388,27 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
     if (L > 0 && (!d_counts || !d_cov || !d_ent || !d_sec)) return fail(BC_E_ARG, "NULL output");
     DeviceGuard g(c->device);
     if (bc::use_rc(*r, L)) {
-        // deep batch: counts by the read-chunked kernel (atomics into zeroed counts), then kernel 2
-        if (L > 0) HIP_TRY(hipMemsetAsync(d_counts, 0, (size_t)k * (size_t)L * 4, c->stream));
+        // deep batch: counts by the read-chunked kernel (atomics into the context's zeroed
+        // scratch), then kernel 2, which also moves the counts to d_counts and re-zeroes the
+        // scratch (no memset launch per call)
+        const size_t need = (size_t)k * (size_t)L * 4;
+        if (need > c->rc_scratch_bytes) {
+            if (c->rc_scratch) {
+                HIP_TRY(hipStreamSynchronize(c->stream));
+                HIP_TRY(hipFree(c->rc_scratch));
+                c->rc_scratch = nullptr;
+                c->rc_scratch_bytes = 0;
+            }
+            HIP_TRY(hipMalloc((void**)&c->rc_scratch, need));
+            c->rc_scratch_bytes = need;
+            HIP_TRY(hipMemsetAsync(c->rc_scratch, 0, need, c->stream));
+        }
         {
             Timed tm(c, BC_K_RC);
-            HIP_TRY(bc::launch_rc(c->stream, *r, L, mbq, k, d_counts, c->d_err));
+            HIP_TRY(bc::launch_rc(c->stream, *r, L, mbq, k, c->rc_scratch, c->d_err));
         }
         Timed tm(c, BC_K_STATS);
-        HIP_TRY(bc::launch_stats(c->stream, d_counts, L, k, nf, nf2, d_cov, d_pc, d_ent, d_sec));
+        HIP_TRY(bc::launch_stats(c->stream, c->rc_scratch, L, k, nf, nf2, d_cov, d_pc, d_ent, d_sec, d_counts));
         return BC_OK;
     }
     Timed tm(c, BC_K_PILEUP);

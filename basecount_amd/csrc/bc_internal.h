@@ -20,6 +20,8 @@ struct bc_ctx {
     bool timing = false;                  // bc_timing_enable: hipEvents around every launch
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[BC_KERNEL_IDS];
     hipEvent_t mark[BC_EVENT_SLOTS] = {};   // bc_event_record slots (created on first use)
+    int32_t* rc_scratch = nullptr;         // bc_pileup's k_rc accumulation buffer, kept zeroed
+    size_t rc_scratch_bytes = 0;
 };
 
 struct bc_graph {
@@ -43,8 +45,10 @@ hipError_t launch_count(hipStream_t s, const bc_reads& r, int64_t ref_len, uint3
 size_t seq_event_bytes(int64_t seq_bytes);
 hipError_t launch_seq_event(hipStream_t s, const uint8_t* src, int64_t nbytes, uint8_t* dst);
 hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span);
+// scratch_counts_out != nullptr: hist is the context's zeroed accumulation scratch; its counts go
+// to scratch_counts_out and it is zeroed again (k_stats)
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2,
-                        int32_t* cov, double* pc, double* ent, double* sec);
+                        int32_t* cov, double* pc, double* ent, double* sec, int32_t* scratch_counts_out = nullptr);
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
                                double* pc, double* ent, double* sec, unsigned long long* d_err);

@@ -246,11 +246,15 @@ __global__ void k_seq_event(const uint8_t* src, int64_t nbytes, uint8_t* dst, in
 // the file is compiled with -ffp-contract=off):
 //   probabilities = count / coverage; percentages = 100 * probability;
 //   entropy = nf * sum([-(x*log2(x)) if x != 0 else 0 ...])  (left to right from int 0)
+//
+// counts_out != NULL: `hist` is the library's accumulation scratch (k_rc adds into it): its
+// counts are copied to counts_out and the scratch is left zeroed for the next launch, which
+// saves the per-step memset.
 template <int K>
-__global__ __launch_bounds__(kStatsThreads) void k_stats(const int32_t* __restrict__ hist, int64_t L, double nf,
-                                                          double nf2, int32_t* __restrict__ cov_out,
-                                                          double* __restrict__ pc, double* __restrict__ ent,
-                                                          double* __restrict__ sec) {
+__global__ __launch_bounds__(kStatsThreads) void k_stats(int32_t* __restrict__ hist, int64_t L, double nf, double nf2,
+                                                          int32_t* __restrict__ counts_out,
+                                                          int32_t* __restrict__ cov_out, double* __restrict__ pc,
+                                                          double* __restrict__ ent, double* __restrict__ sec) {
     for (int64_t p = (int64_t)blockIdx.x * kStatsThreads + threadIdx.x; p < L;
          p += (int64_t)gridDim.x * kStatsThreads) {
         int32_t c[K];
@@ -259,6 +263,13 @@ __global__ __launch_bounds__(kStatsThreads) void k_stats(const int32_t* __restri
         for (int j = 0; j < K; ++j) {
             c[j] = hist[(int64_t)j * L + p];
             cov += c[j];
+        }
+        if (counts_out) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                counts_out[(int64_t)j * L + p] = c[j];
+                hist[(int64_t)j * L + p] = 0;
+            }
         }
         if (cov_out) cov_out[p] = (int32_t)cov;
         if (cov == 0) {
@@ -649,16 +660,17 @@ hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span) {
 }
 
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2, int32_t* cov,
-                        double* pc, double* ent, double* sec) {
+                        double* pc, double* ent, double* sec, int32_t* scratch_counts_out) {
     if (L <= 0) return hipSuccess;
     int64_t blocks = (L + kStatsThreads - 1) / kStatsThreads;
     if (blocks > 256 * 16) blocks = 256 * 16;
+    int32_t* h = const_cast<int32_t*>(hist);  // written only in scratch mode (scratch_counts_out)
     if (k == 5)
-        hipLaunchKernelGGL(k_stats<5>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, hist, L, nf, nf2, cov, pc,
-                           ent, sec);
+        hipLaunchKernelGGL(k_stats<5>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, h, L, nf, nf2,
+                           scratch_counts_out, cov, pc, ent, sec);
     else
-        hipLaunchKernelGGL(k_stats<6>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, hist, L, nf, nf2, cov, pc,
-                           ent, sec);
+        hipLaunchKernelGGL(k_stats<6>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, h, L, nf, nf2,
+                           scratch_counts_out, cov, pc, ent, sec);
     return hipGetLastError();
 }
 

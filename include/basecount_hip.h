@@ -135,8 +135,11 @@ int bc_count(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min
  *   d_counts [k][L] int32 (the reference's baseCounts columns, N only when k == 6),
  *   d_cov, d_pc (may be NULL), d_ent, d_sec  exactly as bc_stats defines them.
  * Deep batches (many reads per tile) and spans > 4096 instead run the read-chunked kernel 1
- * (each read decoded once, per-block LDS histograms, atomic flush into the zeroed counts)
- * followed by kernel 2: three stream-ordered operations, same results.
+ * (each read decoded once, per-block LDS event image / histograms, atomic flush into a
+ * context-owned scratch kept zeroed) followed by kernel 2, which moves the counts to d_counts
+ * and re-zeroes the scratch: two stream-ordered launches, same results.  The scratch grows on
+ * first use for a larger k * ref_len (a synchronizing allocation: make that first call outside
+ * a graph capture).
  * Out-of-range counted events are recorded for bc_range_error() as with bc_count.
  * Overwrites its outputs; async; capturable.                                                   */
 int bc_pileup(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality, int k,

@@ -106,6 +106,78 @@ def test_kernel1_matches_oracle(ctx, monkeypatch, seed, L, n, sort, long_skip, m
         assert np.array_equal(got, exp[:, :ncols].T.astype(np.int32)), (seed, ncols)
 
 
+def shaped_batch(rng, L, n, templates, nfrac=0.02):
+    """Sorted reads whose CIGARs are drawn from `templates` (lists of (op, len)): targets the
+    read-chunked kernel's event image (<= 2 runs from the read start to its end) and the shapes
+    that make a chunk fall back to the run tables."""
+    pos, cigs, seqs, quals = [], [], [], []
+    for _ in range(n):
+        ops = templates[int(rng.integers(0, len(templates)))]
+        span = sum(ln for op, ln in ops if op in (0, 2, 3, 7, 8))
+        q = sum(ln for op, ln in ops if op in (0, 1, 4, 7, 8))
+        codes = synth.ACGT[rng.integers(0, 4, q)]
+        codes[rng.random(q) < nfrac] = rng.choice([15, 0, 5, 3])
+        seqs.append(codes)
+        quals.append(rng.integers(0, 45, q).astype(np.uint8))
+        pos.append(int(rng.integers(0, L - span)))
+        cigs.append(ops)
+    order = np.argsort(pos, kind="stable")
+    pos, cigs = [pos[i] for i in order], [cigs[i] for i in order]
+    seqs, quals = [seqs[i] for i in order], [quals[i] for i in order]
+    nib = np.zeros(len(pos) + 1, np.int64)
+    nib[1:] = np.cumsum([len(s) + (len(s) & 1) for s in seqs])
+    allc = np.zeros(int(nib[-1]) + 2, np.uint8)
+    qual = np.zeros(int(nib[-1]) + 2, np.uint8)
+    for i, (s, q) in enumerate(zip(seqs, quals)):
+        allc[nib[i]: nib[i] + len(s)] = s
+        qual[nib[i]: nib[i] + len(q)] = q
+    seq = ((allc[0::2] << 4) | allc[1::2]).astype(np.uint8)
+    cig_n = np.array([len(c) for c in cigs], np.uint32)
+    cig_beg = np.zeros(len(cigs), np.uint32)
+    cig_beg[1:] = np.cumsum(cig_n)[:-1]
+    cigar = np.array([(ln << 4) | op for c in cigs for op, ln in c], np.uint32)
+    qstart = np.array([c[0][1] if c[0][0] == 4 else 0 for c in cigs], np.int64)
+    return dict(pos=np.array(pos, np.int32), cig_beg=cig_beg, cig_n=cig_n,
+                seq_nib=(nib[:-1] + qstart).astype(np.uint32), cigar=cigar, seq=seq, qual=qual)
+
+
+IMAGE_OK = [[(0, 150)], [(4, 5), (0, 140), (4, 5)], [(0, 70), (2, 2), (0, 78)],
+            [(0, 70), (1, 3), (0, 77)], [(0, 60), (3, 4), (0, 80)], [(0, 40), (7, 10), (8, 1), (0, 99)],
+            [(5, 3), (0, 100), (2, 1), (0, 49), (4, 2)]]
+FALLBACK = [[(2, 3), (0, 147)], [(0, 147), (2, 3)], [(0, 50), (2, 2), (0, 50), (2, 2), (0, 46)],
+            [(0, 100), (3, 5000), (0, 50)], [(1, 4), (0, 146)]]
+
+
+@pytest.mark.parametrize("mix", ["image", "fallback", "mixed"])
+@pytest.mark.parametrize("mbq,ncols", [(0, 5), (20, 6)])
+def test_rc_event_image_shapes(ctx, monkeypatch, mix, mbq, ncols):
+    """Deep sorted batches through k_rc: chunks the event image takes, chunks whose reads start
+    or end with a deletion / have 3 runs / span too many windows (run tables), and both mixed."""
+    monkeypatch.setenv("BC_PILEUP_PATH", "rc")
+    tpl = {"image": IMAGE_OK, "fallback": FALLBACK, "mixed": IMAGE_OK + FALLBACK[:2]}[mix]
+    rng = np.random.default_rng({"image": 31, "fallback": 32, "mixed": 33}[mix])
+    L = 12_000
+    b = shaped_batch(rng, L, 40_000, tpl)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    got, bad = gpu_count(ctx, b, L, mbq, ncols)
+    assert bad == -1
+    assert np.array_equal(got, exp[:, :ncols].T.astype(np.int32)), mix
+
+
+def test_rc_event_image_range_error(ctx, monkeypatch):
+    """A read running past the reference end inside an imaged chunk: the reference's first
+    offending read (std::out_of_range), nothing counted past L."""
+    monkeypatch.setenv("BC_PILEUP_PATH", "rc")
+    rng = np.random.default_rng(34)
+    L = 5_000
+    b = shaped_batch(rng, L + 400, 30_000, IMAGE_OK[:4])
+    exp, (br, _) = O.bcount(L, 0, b)
+    assert br != -1
+    got, bad = gpu_count(ctx, b, L, 0, 5)
+    assert bad == br
+
+
 def test_kernel1_rpb_and_window_paths(ctx, monkeypatch):
     """Same counts whatever the chunking: tiny chunks, huge chunks (global-atomic path)."""
     rng = np.random.default_rng(9)

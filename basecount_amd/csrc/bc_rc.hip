@@ -40,7 +40,7 @@ struct RcGeo {
     static constexpr int kWaves = NT / 64;
 };
 constexpr int kRcChunk = 256;
-constexpr int kImgRows = 24;  // windows an imaged chunk may cover (event image rows)
+constexpr int kImgRows = 23;  // windows an imaged chunk may cover (odd: the image's read stride)
 constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's first base
 #include "bc_walk.h"
 
@@ -166,7 +166,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     using Geo = RcGeo<NT>;
     constexpr int kRcThreads = Geo::kThreads, kRcReads = Geo::kReads, kStage = Geo::kStage, kRcWaves = Geo::kWaves;
     // records (48 B per read) of the run-table walk, or, on the image path, the chunk's event
-    // image: kImgRows window rows x kRcReads reads of BC_SEQ_EVENT words
+    // image: BC_SEQ_EVENT words [read][window row], kImgRows (odd) words per read, so that both
+    // the expansion (lanes = reads, one row) and the accumulation (lanes = rows, one read) hit
+    // 64 different LDS banks
     constexpr int kRecU4 = kRcReads * 3, kImgU4 = kImgRows * kRcReads / 4;
     __shared__ uint4 rec[kRecU4 > kImgU4 ? kRecU4 : kImgU4];
     uint32_t* img = (uint32_t*)rec;
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             if (!simple) {
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row)
-                    if (row < NWc) img[row * kRcReads + tid] = 0u;
+                    if (row < NWc) img[tid * kImgRows + row] = 0u;
             } else {
                 uint32_t p0 = word(f0), p1 = maxrun == 2 ? word(f1) : 0u;
 #pragma unroll
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                         if ((x & bmask) && c0 + tid < bad) bad = c0 + tid;
                         x &= ~bmask;
                     }
-                    img[row * kRcReads + tid] = x;
+                    img[tid * kImgRows + row] = x;
                 }
             }
         }
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const int gr = tid & 31, q = tid >> 5;
             uint32_t blo[6] = {0u, 0u, 0u, 0u, 0u, 0u}, bhi[6] = {0u, 0u, 0u, 0u, 0u, 0u};
             if (!(A.ablate & 4)) {
-                const uint32_t* col = img + (gr < NWc ? gr : 0) * kRcReads + 32 * q;
+                const uint32_t* col = img + 32 * q * kImgRows + (gr < NWc ? gr : 0);
                 Swar W;
 #pragma unroll
                 for (int c = 0; c < 6; ++c) W.a4[c] = 0;
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 };
 #pragma unroll
                 for (int rr = 0; rr < 32; ++rr) {
-                    swar_add<NC>(W, col[rr]);
+                    swar_add<NC>(W, col[rr * kImgRows]);
                     if (rr == 14 || rr == 29) fold();
                 }
                 fold();
@@ -569,9 +571,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 auto events = [&](uint32_t rr) {
                     const int rs = rr < ghi ? (int)rr : 0;
                     uint32_t x;
-                    if (img_path) {
-                        x = img[(int)(gb / 8 - G0w) * kRcReads + rs];
-                    } else if (A.ablate & 256) {
+                    if (A.ablate & 256) {
                         x = rec[rs * 3].x * 0x01010101u;
                     } else if (maxrun <= 1) {
                         x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)

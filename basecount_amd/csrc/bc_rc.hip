@@ -22,6 +22,7 @@
 // there.  Kernel 2 (k_stats) runs afterwards on the counts.
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 
 #include "bc_internal.h"
 
@@ -41,6 +42,7 @@ struct RcGeo {
 };
 constexpr int kRcChunk = 256;
 constexpr int kImgRows = 23;  // windows an imaged chunk may cover (odd: the image's read stride)
+constexpr int kPadW = 24;     // stage pad words on each side (kImgRows + 1, see the image expansion)
 constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's first base
 #include "bc_walk.h"
 
@@ -62,6 +64,13 @@ constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
     } while (0)
 #endif
 [[maybe_unused]] constexpr int kRcPhases = 7;
+
+// k << (m mod 64): v_lshlrev_b64 reads only the low 6 bits of the shift (C's << may not)
+__device__ __forceinline__ unsigned long long shl64_mod64(unsigned long long k, int m) {
+    unsigned long long r;
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "v"(m), "s"(k));
+    return r;
+}
 
 struct RcArgs {
     const int32_t* pos;
@@ -173,7 +182,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     __shared__ uint4 rec[kRecU4 > kImgU4 ? kRecU4 : kImgU4];
     uint32_t* img = (uint32_t*)rec;
     __shared__ int32_t rpos[kRcReads];  // the chunk's read positions (window tables)
-    __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 32];  // + pads
+    __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 8 * kPadW];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
     __shared__ uint32_t red[kRcWaves][8];
     __shared__ uint32_t wlo[kRcWin], whi[kRcWin], wpre[kRcWin + 1];
@@ -181,7 +190,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     __shared__ uint32_t ncx;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, s8 = lane & 7;
-    uint8_t* stage = stage_raw + 16;
+    uint8_t* stage = stage_raw + 4 * kPadW;
     auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     int64_t bad = INT64_MAX;
 
@@ -355,54 +364,69 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const uint32_t sh0 = (uint32_t)(s0 & 7) * 4u, sh1 = (uint32_t)(s1 & 7) * 4u;
             // Stream bits (4 per nibble) from the image's first row: the read is [Z, SP), its
             // first run [Z, B0), the deletions [B0, A1), the second run [A1, SP) (one-run reads:
-            // A1 = B0 = SP).  T(X) = bits of a row below X; row r's window is bits [32r, 32r + 32).
+            // A1 = B0 = SP).  Row r's window is stream bits [32r, 32r + 32).
             const int ob = 32 * i0 + 4 * p7;  // stream bit of the read's reference offset 0
             const int Z = ob, SP = ob + 4 * (int)T.span;
             const int B0 = ob + 4 * (int)T.en[0];
             const int A1 = T.nrun == 2 ? ob + 4 * (int)T.st[1] : SP;
             const int B0e = T.nrun == 2 ? B0 : SP;
-            const int lim = kStage / 4;
-            const int f0 = wb0 - i0, f1 = wb1 - i0;  // stage word of row r: f_k + r (clamped)
-            const uint32_t* sw = (const uint32_t*)stage;
-            auto thr = [](int c) {  // bits below clamp(c, 0, 32)
-                c = c < 0 ? 0 : (c > 32 ? 32 : c);
-                return (uint32_t)(1ull << c) - 1u;
-            };
-            // stage word w (clamped into the stage and its pads); row r's 8 event classes of run k
-            // are the funnel shift of words f_k + r, f_k + r + 1: one new word per row and run
-            auto word = [&](int w) { return sw[w < -1 ? -1 : (w > lim ? lim : w)]; };
-            if (!simple) {
-#pragma unroll
-                for (int row = 0; row < kImgRows; ++row)
-                    if (row < NWc) img[tid * kImgRows + row] = 0u;
-            } else {
-                uint32_t p0 = word(f0), p1 = maxrun == 2 ? word(f1) : 0u;
+            // run k's stage word of row r is f_k + r (+1 for the funnel's upper word): within
+            // [-kPadW + 1, kStage / 4 + kPadW - 1] for every simple read (f_k >= -1 - 22, the
+            // read's sequence lies in the stage), so the stage's pads absorb it unclamped
+            const uint32_t* w0 = (const uint32_t*)stage + (wb0 - i0);
+            const uint32_t* w1 = (const uint32_t*)stage + (wb1 - i0);
+            // Row r's 8 event classes, all rows unrolled without branches so the LDS reads of
+            // later rows issue ahead.  ge(X): the row's stream bits at or above X, i.e. bits
+            // >= d = clamp(X - 32r, 0, 32).  With Y = X - 64 * (r / 2) (one subtraction per row
+            // pair) the clamp is one med3 against inline constants, [0, 32] for even rows and
+            // [32, 64] for odd ones, and 0xFFFFFFFF << (m mod 64) as 64 bits holds the mask in its
+            // low word (even: m = d) or its high word (odd: m = 32 + d, or 0 when d = 32).
+            auto expand = [&](auto two_c, auto edge_c) {
+                constexpr bool TWO = decltype(two_c)::value, EDGE = decltype(edge_c)::value;
+                int yz = Z, yb = B0e, ya = A1, ys = SP;
+                uint32_t p0 = w0[0], p1 = TWO ? w1[0] : 0u;
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) {
-                    if (row >= NWc) continue;  // (uniform)
-                    const int c = 32 * row;
-                    const uint32_t tz = thr(Z - c), tb = thr(B0e - c), ta = thr(A1 - c), ts = thr(SP - c);
-                    const uint32_t n0 = word(f0 + row + 1);
-                    const uint32_t v0 = __builtin_amdgcn_alignbit(n0, p0, sh0);
+                    if (row > 0 && !(row & 1)) yz -= 64, yb -= 64, ya -= 64, ys -= 64;
+                    auto ge = [&](int Y) {
+                        const int lo = (row & 1) ? 32 : 0;
+                        const int m = Y < lo ? lo : (Y > lo + 32 ? lo + 32 : Y);
+                        const unsigned long long v = shl64_mod64(0xFFFFFFFFull, m);
+                        return (row & 1) ? (uint32_t)(v >> 32) : (uint32_t)v;
+                    };
+                    const uint32_t gz = ge(yz), gb = ge(yb);
+                    const uint32_t n0 = w0[row + 1];
+                    uint32_t x = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n0, p0, sh0), gz, gb, 0x40);
                     p0 = n0;
-                    uint32_t x = v0 & tb & ~tz;
-                    if (maxrun == 2) {  // (uniform)
-                        const uint32_t n1 = word(f1 + row + 1);
-                        const uint32_t v1 = __builtin_amdgcn_alignbit(n1, p1, sh1);
+                    if (TWO) {
+                        const uint32_t ga = ge(ya), gs = ge(ys);
+                        const uint32_t n1 = w1[row + 1];
+                        const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n1, p1, sh1), ga, gs, 0x40);
+                        x = x | x1 | __builtin_amdgcn_bitop3_b32(kClsDel, gb, ga, 0x40);  // s0 & s1 & ~s2
                         p1 = n1;
-                        x |= v1 & ts & ~ta;
                     }
-                    if (gap) x |= kClsDel & ta & ~tb;  // (uniform)
-                    const int64_t rb = 8 * (int64_t)(G0 + row);  // (uniform) the row's first position
-                    if (rb + 8 > A.L) {  // events at positions >= L: the reference's out_of_range
-                        int64_t kL = A.L - rb;
-                        kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
-                        const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
-                        if ((x & bmask) && c0 + tid < bad) bad = c0 + tid;
-                        x &= ~bmask;
+                    if (EDGE) {
+                        const int64_t rb = 8 * (int64_t)(G0 + row);  // (uniform) the row's first position
+                        if (rb + 8 > A.L) {  // events at positions >= L: the reference's out_of_range
+                            int64_t kL = A.L - rb;
+                            kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
+                            const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
+                            if ((x & bmask) && c0 + tid < bad) bad = c0 + tid;
+                            x &= ~bmask;
+                        }
                     }
                     img[tid * kImgRows + row] = x;
                 }
+            };
+            if (!simple) {
+#pragma unroll
+                for (int row = 0; row < kImgRows; ++row) img[tid * kImgRows + row] = 0u;
+            } else if (8 * (int64_t)(G0 + kImgRows) > A.L) {  // (uniform) rows may reach past L
+                expand(std::true_type{}, std::true_type{});
+            } else if (maxrun == 2) {
+                expand(std::true_type{}, std::false_type{});
+            } else {
+                expand(std::false_type{}, std::false_type{});
             }
         }
         fetch_fields(chunk + gridDim.x);  // in flight during the walk

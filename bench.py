@@ -242,7 +242,7 @@ def main():
         # eager launches: the kernel's own average duration (what rocprofv3's kernel trace
         # reports); a graph replay hides part of the launch gap and would flatter the roofline
         kern_s["pileup"] = dev_step if graph is None else region(step, max(3, min(args.steps, 100)))
-    else:  # deep batches: memset + k_rc + k_stats (bc_count on the same batch launches k_rc alone)
+    else:  # deep batches: k_rc + k_stats (bc_count on the same batch launches k_rc alone)
         reps = max(3, min(args.steps, 50))
 
         def count_only():
@@ -338,7 +338,7 @@ def main():
             "device_us_per_step": dev_step * 1e6,
             "kernel_us": {kernel_names[n]: v * 1e6 for n, v in kern_s.items()},
             "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per contig per step"
-                        if dom == "pileup" else "memset + k_rc (kernel 1) + k_stats (kernel 2) per contig per step")
+                        if dom == "pileup" else "k_rc (kernel 1, into a zeroed scratch) + k_stats (kernel 2, moves the counts out and re-zeroes) per contig per step")
                        + (", the K timed steps replayed from one hipGraph" if graph is not None else ", eager launches"),
             "parity_vs_oracle": parity,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -36,7 +36,6 @@ constexpr int kCountThreads = 256;
 // LDS window: counts of one chunk's reads, packed two 16-bit columns per 32-bit word
 // (planes {A|C, G|T, DS|N}); a chunk holds < 65536 reads so a 16-bit half never overflows.
 constexpr int kWinMax = 4096;  // positions per window -> 3 * 4096 * 4 B = 48 KiB
-constexpr int kStatsThreads = 256;
 constexpr int kNpBuf = 8192;   // numpy's default ufunc buffer size (reduction chunk)
 
 // launchers (bc_kernels.hip); all async on `s`, return hipError_t

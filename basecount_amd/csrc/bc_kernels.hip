@@ -250,64 +250,81 @@ __global__ void k_seq_event(const uint8_t* src, int64_t nbytes, uint8_t* dst, in
 // counts_out != NULL: `hist` is the library's accumulation scratch (k_rc adds into it): its
 // counts are copied to counts_out and the scratch is left zeroed for the next launch, which
 // saves the per-step memset.
+//
+// One block per 64-position tile, K waves: wave j loads column j of the tile and computes that
+// column's percentage and entropy terms (one division and one log2 per term instead of a chain
+// of K per thread); wave 0 then adds the terms in column order.  The sums are the same
+// left-to-right sequences as main.py:40-53, so the results are unchanged by the split.
 template <int K>
-__global__ __launch_bounds__(kStatsThreads) void k_stats(int32_t* __restrict__ hist, int64_t L, double nf, double nf2,
-                                                          int32_t* __restrict__ counts_out,
-                                                          int32_t* __restrict__ cov_out, double* __restrict__ pc,
-                                                          double* __restrict__ ent, double* __restrict__ sec) {
-    for (int64_t p = (int64_t)blockIdx.x * kStatsThreads + threadIdx.x; p < L;
-         p += (int64_t)gridDim.x * kStatsThreads) {
-        int32_t c[K];
-        int64_t cov = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            c[j] = hist[(int64_t)j * L + p];
-            cov += c[j];
-        }
-        if (counts_out) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                counts_out[(int64_t)j * L + p] = c[j];
+__global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, int64_t L, double nf, double nf2,
+                                                   int32_t* __restrict__ counts_out, int32_t* __restrict__ cov_out,
+                                                   double* __restrict__ pc, double* __restrict__ ent,
+                                                   double* __restrict__ sec) {
+    __shared__ int32_t cnt[K][64];
+    __shared__ double t1[K][64], t2[K][64];
+    const int j = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t n_tiles = (L + 63) / 64;
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t p = tile * 64 + lane;
+        const bool in = p < L;
+        int32_t cj = 0;
+        if (in) {
+            cj = hist[(int64_t)j * L + p];
+            if (counts_out) {
+                counts_out[(int64_t)j * L + p] = cj;
                 hist[(int64_t)j * L + p] = 0;
             }
         }
-        if (cov_out) cov_out[p] = (int32_t)cov;
-        if (cov == 0) {
-            if (pc) {
-#pragma unroll
-                for (int j = 0; j < K; ++j) pc[(int64_t)j * L + p] = -1.0;
-            }
-            if (ent) ent[p] = 1.0;
-            if (sec) sec[p] = 1.0;
-            continue;
-        }
-        const double dcov = (double)cov;
-        double s = 0.0;
+        cnt[j][lane] = cj;
+        __syncthreads();
+        int64_t cov = 0;
         int am = 0;
+        int32_t c[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const double pj = (double)c[j] / dcov;
+        for (int i = 0; i < K; ++i) {
+            c[i] = cnt[i][lane];
+            cov += c[i];
+        }
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            if (c[i] > c[am]) am = i;  // np.argmax: first maximum
+        double e1 = 0.0, e2 = 0.0;
+        if (in && cov != 0) {
+            const double pj = (double)cj / (double)cov;
             if (pc) pc[(int64_t)j * L + p] = 100.0 * pj;
-            if (c[j] != 0) s = s + (-(pj * log2(pj)));
-            if (c[j] > c[am]) am = j;  // np.argmax: first maximum
-        }
-        if (ent) ent[p] = nf * s;
-        if (sec) {
+            if (cj != 0) e1 = -(pj * log2(pj));
             const int64_t cov2 = cov - c[am];
-            double h2 = 1.0;
-            if (cov2 != 0) {
-                const double d2 = (double)cov2;
-                double s2 = 0.0;
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    if (j == am || c[j] == 0) continue;
-                    const double q = (double)c[j] / d2;
-                    s2 = s2 + (-(q * log2(q)));
-                }
-                h2 = nf2 * s2;
+            if (sec && j != am && cj != 0 && cov2 != 0) {
+                const double q = (double)cj / (double)cov2;
+                e2 = -(q * log2(q));
             }
-            sec[p] = h2;
+        } else if (in && pc) {
+            pc[(int64_t)j * L + p] = -1.0;
         }
+        t1[j][lane] = e1;
+        t2[j][lane] = e2;
+        __syncthreads();
+        if (j == 0 && in) {
+            if (cov_out) cov_out[p] = (int32_t)cov;
+            double h = 1.0, h2 = 1.0;
+            if (cov != 0) {
+                double s = 0.0;
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    if (c[i] != 0) s = s + t1[i][lane];
+                h = nf * s;
+                if (cov - c[am] != 0) {
+                    double s2 = 0.0;
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+                        if (i != am && c[i] != 0) s2 = s2 + t2[i][lane];
+                    h2 = nf2 * s2;
+                }
+            }
+            if (ent) ent[p] = h;
+            if (sec) sec[p] = h2;
+        }
+        __syncthreads();  // cnt / t1 / t2 reused by the next tile
     }
 }
 
@@ -662,14 +679,14 @@ hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span) {
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2, int32_t* cov,
                         double* pc, double* ent, double* sec, int32_t* scratch_counts_out) {
     if (L <= 0) return hipSuccess;
-    int64_t blocks = (L + kStatsThreads - 1) / kStatsThreads;
-    if (blocks > 256 * 16) blocks = 256 * 16;
+    int64_t blocks = (L + 63) / 64;  // one 64-position tile per block
+    if (blocks > 256 * 8 * 8) blocks = 256 * 8 * 8;
     int32_t* h = const_cast<int32_t*>(hist);  // written only in scratch mode (scratch_counts_out)
     if (k == 5)
-        hipLaunchKernelGGL(k_stats<5>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, h, L, nf, nf2,
+        hipLaunchKernelGGL(k_stats<5>, dim3((unsigned)blocks), dim3(64 * 5), 0, s, h, L, nf, nf2,
                            scratch_counts_out, cov, pc, ent, sec);
     else
-        hipLaunchKernelGGL(k_stats<6>, dim3((unsigned)blocks), dim3(kStatsThreads), 0, s, h, L, nf, nf2,
+        hipLaunchKernelGGL(k_stats<6>, dim3((unsigned)blocks), dim3(64 * 6), 0, s, h, L, nf, nf2,
                            scratch_counts_out, cov, pc, ent, sec);
     return hipGetLastError();
 }

@@ -387,6 +387,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 uint32_t p0 = w0[0], p1 = TWO ? w1[0] : 0u;
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) {
+                    if (row >= kImgRows - 4 && row >= NWc) continue;  // (uniform) past the chunk
                     if (row > 0 && !(row & 1)) yz -= 64, yb -= 64, ya -= 64, ys -= 64;
                     auto ge = [&](int Y) {
                         const int lo = (row & 1) ? 32 : 0;
@@ -402,6 +403,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                         const uint32_t ga = ge(ya), gs = ge(ys);
                         const uint32_t n1 = w1[row + 1];
                         const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n1, p1, sh1), ga, gs, 0x40);
+                        // (independent terms: a select chain measured slower, 57 vs 54 us)
                         x = x | x1 | __builtin_amdgcn_bitop3_b32(kClsDel, gb, ga, 0x40);  // s0 & s1 & ~s2
                         p1 = n1;
                     }
@@ -438,16 +440,20 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         if (img_path) {
             __syncthreads();  // the image complete (columns are written by their read's thread)
             RC_STAMP(4);
-            // ---- image path, transposed: thread (row g = tid & 31, read group q = tid >> 5) adds
-            // the 32 reads [32q, 32q + 32) of window row g into SWAR nibble counters (zero image
-            // words for reads outside the window), byte counters per class every <= 15 reads.
-            // Lanes g and g + 32 of a wave hold the same row (groups 2w, 2w + 1): summed with a
-            // lane swap; the 4 waves through LDS; thread g < 32 flushes its 8 positions.
-            uint32_t (*part)[2 * 6][32] = (uint32_t (*)[2 * 6][32])&hist[0][0];  // [wave][2 NC][32]
-            const int gr = tid & 31, q = tid >> 5;
-            uint32_t blo[6] = {0u, 0u, 0u, 0u, 0u, 0u}, bhi[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-            if (!(A.ablate & 4)) {
-                const uint32_t* col = img + 32 * q * kImgRows + (gr < NWc ? gr : 0);
+            // ---- image path, transposed: thread t < 8 R (R = NWc rows) takes row g = t mod R and
+            // read group q = t / R, and adds the 32 reads [32q, 32q + 32) of row g into SWAR nibble
+            // counters, byte counters per class every <= 15 reads.  8 R <= 184 threads: the 4th
+            // wave skips the sum (rows as lanes mod 32 left a third of the lanes idle).  The 8
+            // groups' byte counters meet in LDS (the dead stage); thread (class c, row g) adds
+            // them in 16-bit lanes and writes the row's 8 positions.
+            const int R = NWc;
+            const uint32_t inv = (65536u + (uint32_t)R - 1u) / (uint32_t)R;  // t / R = (t * inv) >> 16 (t < 256)
+            constexpr int kPartStride = 24;                                  // >= kImgRows
+            uint32_t* part = (uint32_t*)stage;                              // [q][2 NC][kPartStride]
+            if (tid < 8 * R && !(A.ablate & 4)) {
+                const int q = (int)(((uint32_t)tid * inv) >> 16), gr = tid - q * R;
+                uint32_t blo[6] = {0u, 0u, 0u, 0u, 0u, 0u}, bhi[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+                const uint32_t* col = img + 32 * q * kImgRows + gr;
                 Swar W;
 #pragma unroll
                 for (int c = 0; c < 6; ++c) W.a4[c] = 0;
@@ -465,45 +471,34 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     if (rr == 14 || rr == 29) fold();
                 }
                 fold();
-                if (gr >= NWc) {
-#pragma unroll
-                    for (int c = 0; c < 6; ++c) blo[c] = bhi[c] = 0;
-                }
-            }
-            // bytes <= 64 after the lane swap (two groups of 32 reads)
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                blo[c] += (uint32_t)__shfl_xor((int)blo[c], 32);
-                bhi[c] += (uint32_t)__shfl_xor((int)bhi[c], 32);
-            }
-            if (lane < 32) {
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
-                    part[wave][2 * c][lane] = blo[c];
-                    part[wave][2 * c + 1][lane] = bhi[c];
+                    part[(q * 2 * NC + 2 * c) * kPartStride + gr] = blo[c];
+                    part[(q * 2 * NC + 2 * c + 1) * kPartStride + gr] = bhi[c];
                 }
             }
-            __syncthreads();  // the waves' partial rows
+            __syncthreads();  // the groups' partial rows
             RC_STAMP(5);
             // the rows' final counts in LDS (the image is dead), [class][position]
             uint32_t* fin = img;
-            if (tid < 32 && tid < NWc) {
+            if (tid < NC * R) {
+                const int c = (int)(((uint32_t)tid * inv) >> 16), gr = tid - c * R;
+                // byte k of the lo (hi) word = position 2k (2k + 1); 8 groups x <= 32 fits 16 bits
+                uint32_t e = 0, o = 0, e2 = 0, o2 = 0;
+                if (!(A.ablate & 4)) {
 #pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    // byte k of the lo (hi) word = position 2k (2k + 1); 4 waves x <= 64 fits 16 bits
-                    uint32_t e = 0, o = 0, e2 = 0, o2 = 0;
-#pragma unroll
-                    for (int w = 0; w < kRcWaves; ++w) {
-                        const uint32_t vl = part[w][2 * c][tid], vh = part[w][2 * c + 1][tid];
+                    for (int g8 = 0; g8 < 8; ++g8) {
+                        const uint32_t vl = part[(g8 * 2 * NC + 2 * c) * kPartStride + gr];
+                        const uint32_t vh = part[(g8 * 2 * NC + 2 * c + 1) * kPartStride + gr];
                         e += vl & 0x00FF00FFu;         // positions 0, 4 (16-bit halves)
                         e2 += (vl >> 8) & 0x00FF00FFu;  // positions 2, 6
                         o += vh & 0x00FF00FFu;         // positions 1, 5
                         o2 += (vh >> 8) & 0x00FF00FFu;  // positions 3, 7
                     }
-                    uint32_t* f = fin + c * 8 * kImgRows + 8 * tid;
-                    f[0] = e & 0xFFFFu, f[1] = o & 0xFFFFu, f[2] = e2 & 0xFFFFu, f[3] = o2 & 0xFFFFu;
-                    f[4] = e >> 16, f[5] = o >> 16, f[6] = e2 >> 16, f[7] = o2 >> 16;
                 }
+                uint32_t* f = fin + c * 8 * kImgRows + 8 * gr;
+                f[0] = e & 0xFFFFu, f[1] = o & 0xFFFFu, f[2] = e2 & 0xFFFFu, f[3] = o2 & 0xFFFFu;
+                f[4] = e >> 16, f[5] = o >> 16, f[6] = e2 >> 16, f[7] = o2 >> 16;
             }
             __syncthreads();  // the chunk's counts complete
             // flush: one position per thread, 256 contiguous bytes per atomic wave-instruction

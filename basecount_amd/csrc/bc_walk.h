@@ -40,46 +40,42 @@ struct RunTable {
 };
 
 __device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn, int cmax) {
+    // Branch-free: every op updates the table through selects (a divergent if/else chain here
+    // compiles to hundreds of register moves per read).
     RunTable T;
 #pragma unroll
     for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
-    T.nrun = 0;
-    T.gap = false;
-    T.complex = cn > (uint32_t)kPre;
+    bool cx = cn > (uint32_t)kPre, gap = false;
     uint32_t rc = 0, qc = 0, last_en = 0xFFFFFFFFu;
-    int last_qd = 0;
+    int last_qd = 0, nrun = 0;
 #pragma unroll
     for (int k = 0; k < kPre; ++k) {
         if (k >= cmax) break;  // wave-uniform: no lane has more ops
-        if ((uint32_t)k < cn) {
-            const uint32_t op = w[k] & 15u, len = w[k] >> 4;
-            if (mlike(op) && len) {
-                const int qd = (int)qc - (int)rc;
-                if (qd < -32768 || qd > 32767) T.complex = true;
-                if (last_en == rc && last_qd == qd) {  // extends the previous run
+        const uint32_t op = w[k] & 15u, len = (uint32_t)k < cn ? w[k] >> 4 : 0u;
+        const bool m = mlike(op) && len != 0u;  // M/=/X: a run (new, or extending the last one)
+        const bool d = dlike(op) && len != 0u;  // D/N: reference only
+        const int qd = (int)qc - (int)rc;
+        const bool ext = m && last_en == rc && last_qd == qd;
+        const bool nw = m && !ext;
+        cx = cx || (m && (qd < -32768 || qd > 32767)) || (nw && nrun >= kMaxRuns);
+        const uint32_t e = rc + len;
 #pragma unroll
-                    for (int i = 0; i < kMaxRuns; ++i)
-                        if (T.nrun - 1 == i) T.en[i] = rc + len;
-                } else {
-                    if (T.nrun >= kMaxRuns) T.complex = true;
-#pragma unroll
-                    for (int i = 0; i < kMaxRuns; ++i)
-                        if (T.nrun == i) T.st[i] = rc, T.en[i] = rc + len, T.qd[i] = qd;
-                    ++T.nrun;
-                }
-                rc += len;
-                qc += len;
-                last_en = rc;
-                last_qd = qd;
-            } else if (dlike(op) && len) {
-                T.gap = true;
-                rc += len;
-            } else if (op == 1) {
-                qc += len;
-            }
+        for (int i = 0; i < kMaxRuns; ++i) {
+            const bool sn = nw && nrun == i, se = ext && nrun == i + 1;
+            T.st[i] = sn ? rc : T.st[i];
+            T.qd[i] = sn ? qd : T.qd[i];
+            T.en[i] = (sn || se) ? e : T.en[i];
         }
+        nrun += nw ? 1 : 0;
+        gap = gap || d;
+        rc = (m || d) ? e : rc;
+        qc += (m || op == 1u) ? len : 0u;  // I: query only
+        last_en = m ? e : last_en;
+        last_qd = m ? qd : last_qd;
     }
-    if (rc >= 0x1FFFu) T.complex = true;
+    T.nrun = nrun;
+    T.gap = gap;
+    T.complex = cx || rc >= 0x1FFFu;
     T.span = rc;
     T.qlen = qc;
     return T;

@@ -243,15 +243,19 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
 #pragma unroll
         for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
         const int cmax = (int)U(wave_reduce<true>(valid ? (mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre) : 0u));
-        if (valid) {
-            uint32_t w[kPre];
+        // the first two runs only (all the event image needs); a chunk with more re-decodes below
+        auto decode = [&](auto nslot) {
+            if (valid) {
+                uint32_t w[kPre];
 #pragma unroll
-            for (int i = 0; i < kPre; ++i) {
-                w[i] = 0u;
-                if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
+                for (int i = 0; i < kPre; ++i) {
+                    w[i] = 0u;
+                    if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
+                }
+                T = decode_runs<decltype(nslot)::value>(w, mcn, cmax);
             }
-            T = decode_runs(w, mcn, cmax);
-        }
+        };
+        decode(std::integral_constant<int, 2>{});
         const bool cx = valid && T.complex;
         const bool simple = valid && !cx;
         if (tid == 0) ncx = 0;
@@ -288,6 +292,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const uint32_t seg_hi = v[3];
         const int maxspan = (int)v[4], maxrun = (int)v[5];
         const bool gap = v[6] != 0;
+        if (maxrun > 2) decode(std::integral_constant<int, kMaxRuns>{});  // (uniform) full run tables
         seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
         if (cx) cxl[atomicAdd(&ncx, 1u)] = (uint32_t)tid;
         const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));

@@ -39,6 +39,9 @@ struct RunTable {
     bool complex;
 };
 
+// NSLOT < kMaxRuns fills only the first NSLOT runs' st / en / qd (nrun, complex and the rest are
+// those of the full table): callers re-decode with the full table when a read has more runs.
+template <int NSLOT = kMaxRuns>
 __device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn, int cmax) {
     // Branch-free: every op updates the table through selects (a divergent if/else chain here
     // compiles to hundreds of register moves per read).
@@ -60,7 +63,7 @@ __device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint3
         cx = cx || (m && (qd < -32768 || qd > 32767)) || (nw && nrun >= kMaxRuns);
         const uint32_t e = rc + len;
 #pragma unroll
-        for (int i = 0; i < kMaxRuns; ++i) {
+        for (int i = 0; i < NSLOT; ++i) {
             const bool sn = nw && nrun == i, se = ext && nrun == i + 1;
             T.st[i] = sn ? rc : T.st[i];
             T.qd[i] = sn ? qd : T.qd[i];

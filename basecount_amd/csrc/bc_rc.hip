@@ -382,20 +382,19 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const uint32_t* w1 = (const uint32_t*)stage + (wb1 - i0);
             // Row r's 8 event classes, all rows unrolled without branches so the LDS reads of
             // later rows issue ahead.  ge(X): the row's stream bits at or above X, i.e. bits
-            // >= d = clamp(X - 32r, 0, 32).  With Y = X - 64 * (r / 2) (one subtraction per row
-            // pair) the clamp is one med3 against inline constants, [0, 32] for even rows and
-            // [32, 64] for odd ones, and 0xFFFFFFFF << (m mod 64) as 64 bits holds the mask in its
-            // low word (even: m = d) or its high word (odd: m = 32 + d, or 0 when d = 32).
+            // >= d = clamp(X - 32r, 0, 32).  The clamp is one med3 of X against [32r, 32r + 32]
+            // (constants the compiler keeps in registers), and 0xFFFFFFFF << (m mod 64) as 64
+            // bits holds the mask in its low word (even r: m mod 64 = d) or its high word (odd r:
+            // 32 + d, or 0 when d = 32).
             auto expand = [&](auto two_c, auto edge_c) {
                 constexpr bool TWO = decltype(two_c)::value, EDGE = decltype(edge_c)::value;
-                int yz = Z, yb = B0e, ya = A1, ys = SP;
+                const int yz = Z, yb = B0e, ya = A1, ys = SP;
                 uint32_t p0 = w0[0], p1 = TWO ? w1[0] : 0u;
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) {
                     if (row >= kImgRows - 4 && row >= NWc) continue;  // (uniform) past the chunk
-                    if (row > 0 && !(row & 1)) yz -= 64, yb -= 64, ya -= 64, ys -= 64;
                     auto ge = [&](int Y) {
-                        const int lo = (row & 1) ? 32 : 0;
+                        const int lo = 32 * row;
                         const int m = Y < lo ? lo : (Y > lo + 32 ? lo + 32 : Y);
                         const unsigned long long v = shl64_mod64(0xFFFFFFFFull, m);
                         return (row & 1) ? (uint32_t)(v >> 32) : (uint32_t)v;
@@ -409,7 +408,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                         const uint32_t n1 = w1[row + 1];
                         const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n1, p1, sh1), ga, gs, 0x40);
                         // (independent terms: a select chain measured slower, 57 vs 54 us)
-                        x = x | x1 | __builtin_amdgcn_bitop3_b32(kClsDel, gb, ga, 0x40);  // s0 & s1 & ~s2
+                        // s0 & s1 & ~s2 (0x40); then s0 | s1 | s2 (0xFE) in one op
+                        x = __builtin_amdgcn_bitop3_b32(x, x1, __builtin_amdgcn_bitop3_b32(kClsDel, gb, ga, 0x40), 0xFE);
                         p1 = n1;
                     }
                     if (EDGE) {

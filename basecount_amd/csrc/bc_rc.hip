@@ -211,6 +211,23 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     };
     fetch_fields(blockIdx.x);
 
+    // An image chunk's counts (fin, in the image path's otherwise unused hist region) are flushed
+    // by wave 3 during the NEXT image chunk's sum, in which it has no rows: waves 0-2 then never
+    // issue atomics, and their next CIGAR loads do not wait behind them (vmcnt is in order).
+    uint32_t* const fin = &hist[0][0];  // [class][8 kImgRows positions]
+    static_assert(6 * 8 * kImgRows <= 3 * kRcWinPos, "fin fits the hist region");
+    int pend_g0 = 0, pend_nw = 0;  // (uniform) the pending chunk's first window and window count
+    auto flush_pending = [&](int t0, int stride) {
+        for (int t = t0; t < ((A.ablate & 2048) ? 0 : 8 * pend_nw); t += stride) {
+            const int64_t p = 8 * (int64_t)pend_g0 + t;
+            if (p >= A.L) break;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const uint32_t v = fin[c * 8 * kImgRows + t];
+                if (v) atomicAdd(&A.counts[(int64_t)c * A.L + p], (int32_t)v);
+            }
+        }
+    };
 #ifdef BC_PHASE_TRACE
     uint64_t tsum[kRcPhases] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
 #endif
@@ -481,11 +498,12 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     part[(q * 2 * NC + 2 * c) * kPartStride + gr] = blo[c];
                     part[(q * 2 * NC + 2 * c + 1) * kPartStride + gr] = bhi[c];
                 }
+            } else if (wave == kRcWaves - 1) {
+                flush_pending(lane, 64);  // the previous image chunk's counts (8 R <= 184 < 192)
             }
-            __syncthreads();  // the groups' partial rows
+            __syncthreads();  // the groups' partial rows; the pending counts read
             RC_STAMP(5);
-            // the rows' final counts in LDS (the image is dead), [class][position]
-            uint32_t* fin = img;
+            // the rows' final counts in LDS, [class][position]
             if (tid < NC * R) {
                 const int c = (int)(((uint32_t)tid * inv) >> 16), gr = tid - c * R;
                 // byte k of the lo (hi) word = position 2k (2k + 1); 8 groups x <= 32 fits 16 bits
@@ -505,17 +523,13 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 f[0] = e & 0xFFFFu, f[1] = o & 0xFFFFu, f[2] = e2 & 0xFFFFu, f[3] = o2 & 0xFFFFu;
                 f[4] = e >> 16, f[5] = o >> 16, f[6] = e2 >> 16, f[7] = o2 >> 16;
             }
-            __syncthreads();  // the chunk's counts complete
-            // flush: one position per thread, 256 contiguous bytes per atomic wave-instruction
-            for (int t = tid; t < ((A.ablate & 2048) ? 0 : 8 * NWc); t += kRcThreads) {
-                const int64_t p = 8 * (int64_t)G0w + t;
-                if (p >= A.L) break;
-#pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    const uint32_t v = fin[c * 8 * kImgRows + t];
-                    if (v) atomicAdd(&A.counts[(int64_t)c * A.L + p], (int32_t)v);
-                }
-            }
+            pend_g0 = G0w;  // flushed by wave 3 in the next image chunk, or below
+            pend_nw = NWc;
+        }
+        if (!img_path && pend_nw) {  // (uniform) the run tables reuse hist: flush the pending counts
+            flush_pending(tid, kRcThreads);
+            pend_nw = 0;
+            __syncthreads();
         }
         // ---- 2./3. window passes of up to kRcWin windows (run-table walk)
         for (int64_t wp = 0; wp < (img_path ? 0 : NW); wp += kRcWin) {
@@ -659,6 +673,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         for (int k = 0; k < kRcPhases; ++k)
             A.trace[((size_t)blockIdx.x * kRcWaves + wave) * kRcPhases + k] = tsum[k];
 #endif
+    flush_pending(tid, kRcThreads);  // the last image chunk's counts (written before its end barrier)
     // first offending read of this block (std::out_of_range in the reference)
     for (int o = 32; o > 0; o >>= 1) {
         const int64_t b2 = __shfl_down(bad, o);

@@ -499,6 +499,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     part[(q * 2 * NC + 2 * c + 1) * kPartStride + gr] = bhi[c];
                 }
             } else if (wave == kRcWaves - 1) {
+                static_assert(8 * kImgRows <= 64 * (kRcWaves - 1), "the last wave has no image rows");
                 flush_pending(lane, 64);  // the previous image chunk's counts (8 R <= 184 < 192)
             }
             __syncthreads();  // the groups' partial rows; the pending counts read

@@ -488,7 +488,6 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     uint8_t* stage_all = dyn + (size_t)nw * kRecBytes;
     uint32_t(*fin)[6][kTile] = (uint32_t(*)[6][kTile])(stage_all + (size_t)nw * kStageRegion);
     // aliases of the stage regions, live only after the walk (see pileup_lds_bytes)
-    auto red_of = [&](int w) { return (uint32_t*)(stage_all + (size_t)w * kStageRegion); };
     double* terms_g = (double*)(stage_all + (size_t)(g * S) * kStageRegion);
     const int64_t nblk_tiles = (A.n_tiles + groups - 1) / groups;
     const int64_t L = A.L;
@@ -529,6 +528,10 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
         }
         if (S > 1) {
             if (ws == 0 && lane == 0) rng[g][0] = lo, rng[g][1] = hi;
+            if (ws == 0) {  // the S waves add their counts here after the walk
+#pragma unroll
+                for (int c = 0; c < K; ++c) fin[g][c][lane] = 0u;
+            }
             __syncthreads();
             trace_stamp(A, 1);
             lo = rng[g][0];
@@ -578,17 +581,17 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                 if (lane == 0 && bad != INT64_MAX) atomicMin(A.err, (unsigned long long)bad);
             }
         }
-        // ---- reduce the S waves of the group through LDS
+        // ---- reduce the S waves of the group: LDS atomics into fin (zeroed before the range
+        // barrier), so every wave reads the totals after one barrier
         if (S > 1) {
 #pragma unroll
-            for (int c = 0; c < K; ++c) red_of(wave)[c * kTile + lane] = cnt[c];
+            for (int c = 0; c < K; ++c) atomicAdd(&fin[g][c][lane], cnt[c]);
             __syncthreads();
             trace_stamp(A, 4);
-            if (ws == 0)
-                for (int w2 = wave + 1; w2 < wave + S; ++w2) {
+            if (ws == 0) {
 #pragma unroll
-                    for (int c = 0; c < K; ++c) cnt[c] += red_of(w2)[c * kTile + lane];
-                }
+                for (int c = 0; c < K; ++c) cnt[c] = fin[g][c][lane];
+            }
         }
         const bool own = t < A.n_tiles && t0 < L && !(A.ablate & 16);  // tile holds real positions
         if (ws == 0) {
@@ -599,14 +602,14 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                     if (A.accumulate) cnt[c] += (uint32_t)*dst;
                     *dst = (int32_t)cnt[c];
                 }
-                fin[g][c][lane] = cnt[c];
+                if (S == 1 || A.accumulate) fin[g][c][lane] = cnt[c];
             }
         }
         if (!STATS || (A.ablate & 8)) {
             if (S > 1) __syncthreads();
             continue;
         }
-        __syncthreads();
+        if (S == 1 || A.accumulate) __syncthreads();  // (uniform) fin written by wave 0 above
         trace_stamp(A, 5);
         // ---- fused kernel 2: per-lane fp64 terms, then ordered sums per position
         if (own) tile_terms<K>(A, &fin[g][0][0], terms_g, t0, ws * 64 + lane, S * 64);

@@ -21,6 +21,10 @@ def _load(name: str) -> C.CDLL:
     if lib is not None:
         return lib
     path = os.path.join(_HERE, name)
+    if name == "libbcio.so" and os.environ.get("BASECOUNT_HOST_LIB_DIR"):
+        # host-only code may be swapped for its sanitizer build (scripts/asan.sh); the HIP
+        # library never is
+        path = os.path.join(os.environ["BASECOUNT_HOST_LIB_DIR"], name)
     if not os.path.exists(path):
         raise ImportError(
             f"{name} is not built; run `make -C {os.path.join(_HERE, 'csrc')}` "

@@ -59,11 +59,8 @@ struct DeviceGuard {
 
 // Reads per kernel-1 workgroup: enough workgroups to fill 256 CUs several times over, and few
 // enough reads per chunk that a sorted chunk's positions fit one LDS window.
-int choose_rpb(int64_t n, int64_t L, int max_span, int sorted) {
-    if (const char* e = std::getenv("BC_RPB")) {
-        int v = std::atoi(e);
-        if (v > 0) return std::min(v, 32768);
-    }
+int choose_rpb(int64_t n, int64_t L, int max_span, int sorted, int forced) {
+    if (forced > 0) return std::min(forced, 32768);
     int64_t target = std::min<int64_t>(8192, std::max<int64_t>(32, n / 2048));
     if (!sorted || max_span <= 0 || max_span >= bc::kWinMax || L <= 0) return (int)target;
     const double density = (double)n / (double)L;
@@ -152,6 +149,21 @@ extern "C" {
 const char* bc_last_error(void) { return g_err.c_str(); }
 int bc_abi_version(void) { return BC_ABI_VERSION; }
 
+const char* bc_build_info(void) {
+    return "gfx950"
+#ifdef BC_DIAG
+           " diag=1"
+#else
+           " diag=0"
+#endif
+#ifdef BC_PHASE_TRACE
+           " phase_trace=1"
+#else
+           " phase_trace=0"
+#endif
+        ;
+}
+
 int bc_device_count(int* n) {
     if (!n) return fail(BC_E_ARG, "n is NULL");
     int c = 0;
@@ -216,6 +228,18 @@ int bc_ctx_destroy(bc_ctx* c) {
 int bc_ctx_stream(bc_ctx* c, void** s) {
     if (!c || !s) return fail(BC_E_ARG, "NULL argument");
     *s = (void*)c->stream;
+    return BC_OK;
+}
+
+int bc_ctx_set_shape(bc_ctx* c, int shape, int tile_waves, int rpb) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    if (shape < BC_SHAPE_AUTO || shape > BC_SHAPE_TILE_NO_SOLO) return fail(BC_E_ARG, "unknown BC_SHAPE_* value");
+    if (tile_waves != 0 && tile_waves != 1 && tile_waves != 2 && tile_waves != 4 && tile_waves != 8)
+        return fail(BC_E_ARG, "tile_waves must be 0, 1, 2, 4 or 8");
+    if (rpb < 0 || rpb > 32768) return fail(BC_E_ARG, "reads_per_block must be 0..32768");
+    c->shape = shape;
+    c->tile_waves = tile_waves;
+    c->reads_per_block = rpb;
     return BC_OK;
 }
 
@@ -301,13 +325,6 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
         total += (sz[i] + 4095) / 4096 * 4096;
     }
     total = (total + (2u << 20) - 1) / (2u << 20) * (2u << 20);
-    if (std::getenv("BC_SLAB_PAD")) {  // diagnostic: arrays 2 MiB apart
-        total = 0;
-        for (int i = 0; i < 7; ++i) {
-            off[i] = total;
-            total += (sz[i] + (2u << 20) - 1) / (2u << 20) * (2u << 20);
-        }
-    }
     void* slab = nullptr;
     HIP_TRY(hipMalloc(&slab, total));
     for (int i = 0; i < 7; ++i) {
@@ -356,7 +373,7 @@ int bc_count(bc_ctx* c, const bc_reads* r, int64_t ref_len, uint32_t mbq, int nc
     if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
     DeviceGuard g(c->device);
     const bool event = r->seq_layout == BC_SEQ_EVENT && !((uintptr_t)r->seq & 15u);
-    if (r->sorted && event && bc::use_rc(*r, ref_len)) {
+    if (r->sorted && event && bc::use_rc(*r, ref_len, c->shape)) {
         Timed tm(c, BC_K_RC);
         HIP_TRY(bc::launch_rc(c->stream, *r, ref_len, mbq, ncols, d_hist, c->d_err));
         return BC_OK;
@@ -365,10 +382,11 @@ int bc_count(bc_ctx* c, const bc_reads* r, int64_t ref_len, uint32_t mbq, int nc
         // sorted batch: the tiled kernel in accumulate mode (plain read-add-write per owned tile)
         Timed tm(c, BC_K_PILEUP);
         HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, ref_len, r->max_end, mbq, ncols, false, true, 0.0, 0.0,
-                                        d_hist, nullptr, nullptr, nullptr, nullptr, c->d_err));
+                                        d_hist, nullptr, nullptr, nullptr, nullptr, c->d_err, c->shape,
+                                        c->tile_waves));
         return BC_OK;
     }
-    const int rpb = choose_rpb(r->n_reads, ref_len, r->max_span, r->sorted);
+    const int rpb = choose_rpb(r->n_reads, ref_len, r->max_span, r->sorted, c->reads_per_block);
     Timed tm(c, BC_K_COUNT);
     HIP_TRY(bc::launch_count(c->stream, *r, ref_len, mbq, ncols, d_hist, rpb, c->d_err));
     return BC_OK;
@@ -387,7 +405,7 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
         return fail(BC_E_ARG, "bc_pileup needs a 16-byte aligned sequence buffer");
     if (L > 0 && (!d_counts || !d_cov || !d_ent || !d_sec)) return fail(BC_E_ARG, "NULL output");
     DeviceGuard g(c->device);
-    if (bc::use_rc(*r, L)) {
+    if (bc::use_rc(*r, L, c->shape)) {
         // deep batch: counts by the read-chunked kernel (atomics into the context's zeroed
         // scratch), then kernel 2, which also moves the counts to d_counts and re-zeroes the
         // scratch (no memset launch per call)
@@ -413,7 +431,7 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
     }
     Timed tm(c, BC_K_PILEUP);
     HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, d_counts, d_cov,
-                                    d_pc, d_ent, d_sec, c->d_err));
+                                    d_pc, d_ent, d_sec, c->d_err, c->shape, c->tile_waves));
     return BC_OK;
 }
 

@@ -22,7 +22,19 @@ struct bc_ctx {
     hipEvent_t mark[BC_EVENT_SLOTS] = {};   // bc_event_record slots (created on first use)
     int32_t* rc_scratch = nullptr;         // bc_pileup's k_rc accumulation buffer, kept zeroed
     size_t rc_scratch_bytes = 0;
+    // kernel-shape overrides (bc_ctx_set_shape); 0 = chosen from the batch
+    int shape = BC_SHAPE_AUTO;
+    int tile_waves = 0;
+    int reads_per_block = 0;
 };
+
+// Diagnostic work-skipping switches (BC_ABLATE) exist only in -DBC_DIAG builds
+// (scripts/ablate.sh); the shipped library compiles them out.
+#ifdef BC_DIAG
+#define BC_ABL(A) ((A).ablate)
+#else
+#define BC_ABL(A) 0
+#endif
 
 struct bc_graph {
     hipGraph_t graph = nullptr;
@@ -48,15 +60,17 @@ hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span);
 // to scratch_counts_out and it is zeroed again (k_stats)
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2,
                         int32_t* cov, double* pc, double* ent, double* sec, int32_t* scratch_counts_out = nullptr);
+// shape: BC_SHAPE_*; tile_waves: 0 = from the depth, else 1/2/4/8 waves per tile
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
-                               double* pc, double* ent, double* sec, unsigned long long* d_err);
+                               double* pc, double* ent, double* sec, unsigned long long* d_err, int shape = 0,
+                               int tile_waves = 0);
 hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, int ncols, int32_t* counts,
                      unsigned long long* d_err);
 // bc_pileup / bc_count choose the read-chunked k_rc over the tiled k_pileup when a tile would
-// walk at least this many reads (deep batches; BC_PILEUP_PATH=tile|rc overrides)
+// walk at least this many reads (deep batches; bc_ctx_set_shape overrides)
 constexpr double kRcMinReadsPerTile = 2048.0;
-bool use_rc(const bc_reads& r, int64_t L);
+bool use_rc(const bc_reads& r, int64_t L, int shape);
 constexpr int kTileMaxSpan = 4096;  // beyond this span the tiled kernel's look-back gets too long
 size_t summary_work_bytes(int64_t L);
 hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,

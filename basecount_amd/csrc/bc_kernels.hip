@@ -330,7 +330,7 @@ __global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, in
 
 // ------------------------------------------------------------------------------ numpy sums
 // numpy float64 add.reduce (numpy 2.2, verified against np.add.reduce / np.mean in
-// tests/test_npsum.py): the input is consumed in 8192-element buffers, s = 0; s += pw(buffer),
+// test_summary_matches_numpy in tests/test_gpu_parity.py): the input is consumed in 8192-element buffers, s = 0; s += pw(buffer),
 // where pw is numpy's pairwise_sum: n < 8 -> sequential from 0.0; n <= 128 -> eight strided
 // accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail sequentially;
 // else split at n2 = n/2 - (n/2)%8 and add the halves.

@@ -391,10 +391,10 @@ __device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, i
         w[i] = 0u;
         if (lane < nr && i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
     }
-    const bool dma = !QUAL && !(A.ablate & 32);
+    const bool dma = !QUAL && !(BC_ABL(A) & 32);
     uint32_t spec_lo = 0, spec_hi = 0;
     bool spec = false;
-    if (dma && !(A.ablate & 512)) {
+    if (dma && !(BC_ABL(A) & 512)) {
         const uint32_t buf_end = (uint32_t)(A.seq_words * 4 < 0xFFFFFFFFll ? A.seq_words * 4 : 0xFFFFFFF0ll);
         spec_lo = (rdl(msn, 0) >> 1) & ~15u;
         spec_hi = (rdl(msn, nr - 1) >> 1) + kSpecSlack;
@@ -417,7 +417,7 @@ __device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, i
     seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
     const bool spec_ok = spec && !cx && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
     if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
-    const bool staged = !cx && (spec_ok || seg_hi - seg_lo <= (uint32_t)kStage) && !(A.ablate & 32);
+    const bool staged = !cx && (spec_ok || seg_hi - seg_lo <= (uint32_t)kStage) && !(BC_ABL(A) & 32);
     if (spec && !spec_ok) stage_wait();  // the speculative copy must land before it is overwritten
     if (staged && !spec_ok) {
         if (dma) stage_dma<64>(mystage, A.seq + seg_lo, seg_hi - seg_lo, lane);
@@ -441,7 +441,7 @@ __device__ __forceinline__ void process_chunk(const PileArgs& A, int64_t base, i
     F = load_fields(A, next_base, next_nr, lane);  // in flight during the walk
     __builtin_amdgcn_wave_barrier();
     const int64_t rbase = base;
-    if (A.ablate & 4) {
+    if (BC_ABL(A) & 4) {
     } else if (cx) {
         if (pending + nr >= (1 << kField) - 1) {
             flush_acc(acc, cnt);
@@ -476,7 +476,7 @@ template <bool QUAL, int K, bool STATS>
 __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     __shared__ int64_t rng[8][2];  // per group: the tile's read range
-    if (A.ablate & 64) return;
+    if (BC_ABL(A) & 64) return;
     trace_stamp(A, 0);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
         // the tile's reads [lo, hi): searched by the group's first wave (the S waves would all
         // find the same range), handed to the others through LDS
         int64_t lo = 0, hi = 0;
-        if (ws == 0 && t < A.n_tiles && !(A.ablate & 2)) {
+        if (ws == 0 && t < A.n_tiles && !(BC_ABL(A) & 2)) {
 #ifdef BC_PHASE_TRACE
             if (A.trace) {  // diagnostic: latency of one dependent global load from here
                 const int32_t probe = A.pos[(lane * 1543) % (int)A.n];
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             hi = rng[g][1];
         }
         if (t < A.n_tiles) {
-            if (A.ablate & 1) hi = lo;
+            if (BC_ABL(A) & 1) hi = lo;
             const bool edge = t0 + kTile > L;  // uniform
             const bool beyond = P >= L;
             uint32_t bmask = 0;                // window nibbles at positions >= L
@@ -593,7 +593,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                 for (int c = 0; c < K; ++c) cnt[c] = fin[g][c][lane];
             }
         }
-        const bool own = t < A.n_tiles && t0 < L && !(A.ablate & 16);  // tile holds real positions
+        const bool own = t < A.n_tiles && t0 < L && !(BC_ABL(A) & 16);  // tile holds real positions
         if (ws == 0) {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                 if (S == 1 || A.accumulate) fin[g][c][lane] = cnt[c];
             }
         }
-        if (!STATS || (A.ablate & 8)) {
+        if (!STATS || (BC_ABL(A) & 8)) {
             if (S > 1) __syncthreads();
             continue;
         }
@@ -780,7 +780,7 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
                 if (lane == 0 && bad != INT64_MAX) atomicMin(A.err, (unsigned long long)bad);
             }
         }
-        if (t0 < L && P < L && !(A.ablate & 16)) {
+        if (t0 < L && P < L && !(BC_ABL(A) & 16)) {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
                 int32_t* dst = A.counts + (int64_t)c * L + P;
@@ -815,7 +815,8 @@ PileArgs make_args(const bc_reads& r, int64_t L, uint32_t mbq) {
 
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
-                               double* pc, double* ent, double* sec, unsigned long long* d_err) {
+                               double* pc, double* ent, double* sec, unsigned long long* d_err, int shape,
+                               int tile_waves) {
     PileArgs A = make_args(r, L, mbq);
     const int64_t reach = max_end > L ? max_end : L;  // edge tiles up to the furthest read end
     A.n_tiles = (reach + kTile - 1) / kTile;
@@ -829,15 +830,17 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
     A.ent = ent;
     A.sec = sec;
     A.err = d_err;
+#ifdef BC_DIAG
     if (const char* ab = std::getenv("BC_ABLATE")) A.ablate = std::atoi(ab);
+#endif
     // waves per tile from the mean number of reads a tile walks
     // reads overlapping a tile ~ density * (span + 63); aim for ~48 reads per wave
     const double per_tile = reach > 0 ? (double)r.n_reads * (double)(r.max_span + kTile - 1) / (double)reach : 0.0;
     int S = 1;
     while (S < 8 && per_tile > 48.0 * S) S *= 2;
-    if (const char* e = std::getenv("BC_TILE_WAVES")) S = std::max(1, std::min(8, std::atoi(e)));
+    if (tile_waves == 1 || tile_waves == 2 || tile_waves == 4 || tile_waves == 8) S = tile_waves;
     A.S = S;
-    if (S == 1 && !std::getenv("BC_NO_SOLO")) {
+    if (S == 1 && shape != BC_SHAPE_TILE_NO_SOLO) {
         // sparse: waves sweep contiguous tile runs; ~2 rounds of resident waves (256 CUs x 16)
         const int nw = 4;
         const int64_t target_waves = 256 * 16 * 2;

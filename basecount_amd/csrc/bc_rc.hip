@@ -218,7 +218,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     static_assert(6 * 8 * kImgRows <= 3 * kRcWinPos, "fin fits the hist region");
     int pend_g0 = 0, pend_nw = 0;  // (uniform) the pending chunk's first window and window count
     auto flush_pending = [&](int t0, int stride) {
-        for (int t = t0; t < ((A.ablate & 2048) ? 0 : 8 * pend_nw); t += stride) {
+        for (int t = t0; t < ((BC_ABL(A) & 2048) ? 0 : 8 * pend_nw); t += stride) {
             const int64_t p = 8 * (int64_t)pend_g0 + t;
             if (p >= A.L) break;
 #pragma unroll
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         uint32_t spec_hi = (U(fsn_last) >> 1) + kSpecSlack;
         const uint32_t buf_end = (uint32_t)(A.seq_words * 4 < 0xFFFFFFFFll ? A.seq_words * 4 : 0xFFFFFFFFll);
         spec_hi = spec_hi < buf_end ? spec_hi : buf_end;
-        const bool spec = !QUAL && spec_hi > spec_lo && spec_hi - spec_lo <= (uint32_t)kStage && !(A.ablate & 512);
+        const bool spec = !QUAL && spec_hi > spec_lo && spec_hi - spec_lo <= (uint32_t)kStage && !(BC_ABL(A) & 512);
         if (spec) stage_dma<kRcThreads>(stage, A.seq + spec_lo, spec_hi - spec_lo, tid);
         RunTable T;
         T.nrun = 0;
@@ -320,14 +320,14 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // instead of once per (window, run) item from the run table.
         const int64_t WBc = P0 & ~(int64_t)7;
         const int NWc = (int)(P1 > WBc ? (P1 - WBc + 7) / 8 : 0);
-        const bool img_path = staged && maxrun <= 2 && NWc <= kImgRows && !(A.ablate & 8192);
+        const bool img_path = staged && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
         if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
             stage_wait();
             __syncthreads();
         }
         // ---- stage the chunk's sequence exactly (16 B per thread per pass) unless done above
-        if (!QUAL && staged && !spec_ok && !(A.ablate & 512)) stage_dma<kRcThreads>(stage, A.seq + seg_lo, seg_hi - seg_lo, tid);
-        if (QUAL && staged && !spec_ok && !(A.ablate & 512)) {
+        if (!QUAL && staged && !spec_ok && !(BC_ABL(A) & 512)) stage_dma<kRcThreads>(stage, A.seq + seg_lo, seg_hi - seg_lo, tid);
+        if (QUAL && staged && !spec_ok && !(BC_ABL(A) & 512)) {
             for (uint32_t off = tid * 16u; off < seg_hi - seg_lo; off += kRcThreads * 16u) {
                 uint4 q4 = *(const uint4*)(A.seq + seg_lo + off);  // padded buffer: in bounds
                 if (QUAL) {
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const uint32_t inv = (65536u + (uint32_t)R - 1u) / (uint32_t)R;  // t / R = (t * inv) >> 16 (t < 256)
             constexpr int kPartStride = 24;                                  // >= kImgRows
             uint32_t* part = (uint32_t*)stage;                              // [q][2 NC][kPartStride]
-            if (tid < 8 * R && !(A.ablate & 4)) {
+            if (tid < 8 * R && !(BC_ABL(A) & 4)) {
                 const int q = (int)(((uint32_t)tid * inv) >> 16), gr = tid - q * R;
                 uint32_t blo[6] = {0u, 0u, 0u, 0u, 0u, 0u}, bhi[6] = {0u, 0u, 0u, 0u, 0u, 0u};
                 const uint32_t* col = img + 32 * q * kImgRows + gr;
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 const int c = (int)(((uint32_t)tid * inv) >> 16), gr = tid - c * R;
                 // byte k of the lo (hi) word = position 2k (2k + 1); 8 groups x <= 32 fits 16 bits
                 uint32_t e = 0, o = 0, e2 = 0, o2 = 0;
-                if (!(A.ablate & 4)) {
+                if (!(BC_ABL(A) & 4)) {
 #pragma unroll
                     for (int g8 = 0; g8 < 8; ++g8) {
                         const uint32_t vl = part[(g8 * 2 * NC + 2 * c) * kPartStride + gr];
@@ -591,10 +591,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             int g = 0, it4 = 0;
             while (g + 1 < nwin && U(wpre[g + 1]) <= k0) ++g;
             uint32_t gnext = U(wpre[g + 1]), gpre = U(wpre[g]), glo = U(wlo[g]), ghi = U(whi[g]);
-            const uint32_t k1w = (A.ablate & 4) ? k0 : k1;
+            const uint32_t k1w = (BC_ABL(A) & 4) ? k0 : k1;
             for (uint32_t k = k0; k < k1w; ++k) {
                 if (k >= gnext) {  // next window (wave-uniform)
-                    if (it4) rc_fold<NC>(W, hist, g, s8, A.ablate);
+                    if (it4) rc_fold<NC>(W, hist, g, s8, BC_ABL(A));
                     it4 = 0;
                     while (k >= U(wpre[g + 1])) ++g;
                     gnext = U(wpre[g + 1]);
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 auto events = [&](uint32_t rr) {
                     const int rs = rr < ghi ? (int)rr : 0;
                     uint32_t x;
-                    if (A.ablate & 256) {
+                    if (BC_ABL(A) & 256) {
                         x = rec[rs * 3].x * 0x01010101u;
                     } else if (maxrun <= 1) {
                         x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
@@ -643,14 +643,14 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     ++it4;
                 }
                 if (++it4 >= 13) {  // every nibble counter <= 14
-                    rc_fold<NC>(W, hist, g, s8, A.ablate);
+                    rc_fold<NC>(W, hist, g, s8, BC_ABL(A));
                     it4 = 0;
                 }
             }
-            if (it4) rc_fold<NC>(W, hist, g, s8, A.ablate);
+            if (it4) rc_fold<NC>(W, hist, g, s8, BC_ABL(A));
             __syncthreads();
             // ---- 4. flush the pass's positions (< L) into the counts
-            for (int t = tid; t < ((A.ablate & 2048) ? 0 : 8 * nwin); t += kRcThreads) {
+            for (int t = tid; t < ((BC_ABL(A) & 2048) ? 0 : 8 * nwin); t += kRcThreads) {
                 const int64_t p = PB + t;
                 if (p >= A.L) break;
 #pragma unroll
@@ -685,12 +685,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
 
 }  // namespace
 
-bool use_rc(const bc_reads& r, int64_t L) {
+bool use_rc(const bc_reads& r, int64_t L, int shape) {
     if (!r.sorted || r.n_reads <= 0 || r.seq_layout != BC_SEQ_EVENT) return false;
-    if (const char* e = std::getenv("BC_PILEUP_PATH")) {
-        if (!std::strcmp(e, "rc")) return true;
-        if (!std::strcmp(e, "tile")) return r.max_span > kTileMaxSpan;
-    }
+    if (shape == BC_SHAPE_RC) return true;
+    if (shape == BC_SHAPE_TILE || shape == BC_SHAPE_TILE_NO_SOLO) return r.max_span > kTileMaxSpan;
     if (r.max_span > kTileMaxSpan) return true;  // the tiled kernel's look-back gets too long
     const int64_t reach = r.max_end > L ? r.max_end : L;
     const double per_tile = reach > 0 ? (double)r.n_reads * (double)(r.max_span + 63) / (double)reach : 0.0;
@@ -716,7 +714,9 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     A.counts = counts;
     A.err = d_err;
     A.ablate = 0;
+#ifdef BC_DIAG
     if (const char* ab = std::getenv("BC_ABLATE")) A.ablate = std::atoi(ab);
+#endif
     constexpr int nt = kRcChunk;
     A.n_chunks = (r.n_reads + nt - 1) / nt;
     // resident blocks: LDS bounds a CU to 3 (event image + stage + histogram)

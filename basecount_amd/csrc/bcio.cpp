@@ -320,11 +320,14 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
         if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
             return fail(BCIO_E_FORMAT, "not a BGZF file (bad gzip magic / no FEXTRA)");
         uint16_t xlen = rd16(h + 10);
+        // the extra field itself must lie inside the file before any subfield is read
+        if ((uint64_t)12 + xlen > comp_n - off) return fail(BCIO_E_FORMAT, "truncated BGZF extra field");
         uint64_t bsize = 0;
         bool found = false;
         for (uint32_t x = 0; x + 4 <= xlen;) {
             const uint8_t* sf = h + 12 + x;
             uint16_t slen = rd16(sf + 2);
+            if ((uint64_t)x + 4 + slen > xlen) return fail(BCIO_E_FORMAT, "BGZF subfield past the extra field");
             if (sf[0] == 66 && sf[1] == 67 && slen == 2) {
                 bsize = (uint64_t)rd16(sf + 4) + 1;
                 found = true;
@@ -332,11 +335,15 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
             x += 4 + slen;
         }
         if (!found) return fail(BCIO_E_FORMAT, "BGZF block without BC subfield");
+        // header (12 + xlen) + deflate data + CRC32 + ISIZE (8): a smaller BSIZE would underflow
+        // the compressed length handed to the inflater
+        if (bsize < (uint64_t)12 + xlen + 8) return fail(BCIO_E_FORMAT, "BGZF block size smaller than its header");
         if (off + bsize > comp_n) return fail(BCIO_E_FORMAT, "truncated BGZF block");
         Block b;
         b.coff = off + 12 + xlen;
         b.clen = bsize - xlen - 20;
         b.isize = rd32(comp + off + bsize - 4);
+        if (b.isize > 65536) return fail(BCIO_E_FORMAT, "BGZF block inflates past 64 KiB");
         b.uoff = uoff;
         uoff += b.isize;
         blocks.push_back(b);
@@ -437,9 +444,12 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
         const uint8_t* r = p + q + 4;
         int32_t ls = rd32s(r + 16);
         if (ls < 0) return bad("negative l_seq");
+        // the fields must fit the record before their sizes feed the output allocations
+        if (32ull + r[8] + 4ull * rd16(r + 12) + (((uint64_t)ls + 1) / 2) + (uint64_t)ls > bs)
+            return bad("BAM record shorter than its fields");
         starts.push_back(q);
         cig_tot += rd16(r + 12);
-        seq_tot += (uint64_t)((ls + 1) / 2);
+        seq_tot += (((uint64_t)ls + 1) / 2);
         f->cig_off.push_back(cig_tot);
         f->seq_off.push_back(seq_tot);
         q += 4 + (uint64_t)bs;
@@ -468,7 +478,7 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
             uint8_t lrn = r[8], mq = r[9];
             uint16_t nc = rd16(r + 12), fl = rd16(r + 14);
             int32_t ls = rd32s(r + 16);
-            uint64_t need = 32 + (uint64_t)lrn + 4ull * nc + (uint64_t)((ls + 1) / 2) + (uint64_t)ls;
+            uint64_t need = 32 + (uint64_t)lrn + 4ull * nc + (((uint64_t)ls + 1) / 2) + (uint64_t)ls;
             if (need > bs) {
                 ferr = 1;
                 continue;
@@ -488,7 +498,7 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
             }
             f->ref_span[i] = span;
             const uint8_t* s = c + 4ull * nc;
-            uint64_t sb = (uint64_t)((ls + 1) / 2);
+            uint64_t sb = (((uint64_t)ls + 1) / 2);
             std::memcpy(f->seq.data() + f->seq_off[i], s, sb);
             const uint8_t* ql = s + sb;
             uint8_t* qd = f->qual.data() + 2 * f->seq_off[i];
@@ -698,7 +708,7 @@ extern "C" int bcio_write_bam(const char* path, const bcio_write_spec* s) {
         int ln = std::snprintf(name, sizeof name, "r%lld", (long long)i) + 1;
         uint32_t nc = (uint32_t)(s->cig_off[i + 1] - s->cig_off[i]);
         int32_t ls = s->l_seq[i];
-        uint64_t sb = (uint64_t)((ls + 1) / 2);
+        uint64_t sb = (((uint64_t)ls + 1) / 2);
         uint32_t bs = (uint32_t)(32 + ln + 4 * nc + sb + (uint64_t)ls);
         const uint32_t* cg = s->cigar + s->cig_off[i];
         int64_t span = 0;

@@ -16,6 +16,7 @@ from ._native import _libs, _load
 
 BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV = -1, -2, -3, -4
 BC_SEQ_BAM, BC_SEQ_EVENT = 0, 1
+SHAPES = {"auto": 0, "tile": 1, "rc": 2, "tile_no_solo": 3}  # BC_SHAPE_*
 KERNEL_NAMES = ("count", "stats", "rc", "pileup", "summary", "amplicons")  # BC_K_* ids
 KERNEL_IDS = len(KERNEL_NAMES)
 
@@ -56,11 +57,13 @@ def lib() -> C.CDLL:
     sig = {
         "bc_last_error": ([], C.c_char_p),
         "bc_abi_version": ([], C.c_int),
+        "bc_build_info": ([], C.c_char_p),
         "bc_device_count": ([C.POINTER(C.c_int)], C.c_int),
         "bc_ctx_create": ([C.c_int, vp, C.POINTER(vp)], C.c_int),
         "bc_ctx_destroy": ([vp], C.c_int),
         "bc_ctx_stream": ([vp, C.POINTER(vp)], C.c_int),
         "bc_sync": ([vp], C.c_int),
+        "bc_ctx_set_shape": ([vp, C.c_int, C.c_int, C.c_int], C.c_int),
         "bc_malloc": ([vp, C.c_size_t, C.POINTER(vp)], C.c_int),
         "bc_free": ([vp, vp], C.c_int),
         "bc_memcpy_h2d": ([vp, vp, vp, C.c_size_t], C.c_int),
@@ -99,6 +102,11 @@ def lib() -> C.CDLL:
 def check(rc: int) -> None:
     if rc != 0:
         raise BcError(rc, lib().bc_last_error().decode(errors="replace"))
+
+
+def build_info() -> str:
+    """bc_build_info(): e.g. "gfx950 diag=0 phase_trace=0"."""
+    return lib().bc_build_info().decode()
 
 
 def device_count() -> int:
@@ -209,6 +217,11 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_shape(self, shape: str = "auto", tile_waves: int = 0, reads_per_block: int = 0) -> None:
+        """Kernel-shape override for bc_count / bc_pileup (bc_ctx_set_shape): "auto", "tile",
+        "rc" or "tile_no_solo"; tile_waves 0/1/2/4/8; reads_per_block 0 or 1..32768."""
+        check(lib().bc_ctx_set_shape(self.h, SHAPES[shape], int(tile_waves), int(reads_per_block)))
 
     def sync(self):
         check(lib().bc_sync(self.h))

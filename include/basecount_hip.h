@@ -41,7 +41,7 @@ extern "C" {
 #define BC_E_RANGE (-3) /* a counted event fell outside [0, refLen) (count.cpp:60-65,85 .at())   */
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
 
-#define BC_ABI_VERSION 2
+#define BC_ABI_VERSION 3
 
 /* Layouts of bc_reads.seq.
  *   BC_SEQ_BAM   BAM packing: "=ACMGRSVTWYHKDBN" codes, two per byte, high nibble first
@@ -87,6 +87,9 @@ typedef struct bc_ctx bc_ctx;
 
 const char* bc_last_error(void);
 int bc_abi_version(void);
+/* Build description, e.g. "gfx950 diag=0 phase_trace=0": diag=1 marks a diagnostic build whose
+ * kernels can skip work on request (BC_ABLATE); bench.py refuses to report numbers from one.    */
+const char* bc_build_info(void);
 int bc_device_count(int* n);
 
 /* Create a context on `device`.  `stream` is a hipStream_t (NULL: the library creates and owns
@@ -94,6 +97,22 @@ int bc_device_count(int* n);
 int bc_ctx_create(int device, void* stream, bc_ctx** out);
 int bc_ctx_destroy(bc_ctx* ctx);
 int bc_ctx_stream(bc_ctx* ctx, void** stream);
+
+/* Kernel-shape selection for bc_count / bc_pileup on this context (parity tests and tuning; no
+ * shape skips work, every one computes the same counts).  The default, BC_SHAPE_AUTO, picks
+ * from the batch's depth:
+ *   BC_SHAPE_TILE         tiled k_pileup, or its sparse sweep k_pileup_solo (read-chunked k_rc
+ *                         only for spans > 4096)
+ *   BC_SHAPE_RC           read-chunked k_rc (+ k_stats) for every sorted batch
+ *   BC_SHAPE_TILE_NO_SOLO tiled k_pileup, never the sparse sweep
+ * tile_waves: 0 = from the depth, else 1, 2, 4 or 8 waves per 64-position tile (BC_E_ARG
+ * otherwise).  reads_per_block: 0 = automatic, else 1..32768 reads per k_count workgroup
+ * (unsorted batches).                                                                          */
+#define BC_SHAPE_AUTO 0
+#define BC_SHAPE_TILE 1
+#define BC_SHAPE_RC 2
+#define BC_SHAPE_TILE_NO_SOLO 3
+int bc_ctx_set_shape(bc_ctx* ctx, int shape, int tile_waves, int reads_per_block);
 int bc_sync(bc_ctx* ctx);
 
 /* Library-owned device memory helpers (for hosts without another allocator). */

@@ -31,7 +31,8 @@ _lib = None
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
-        path = os.path.join(HERE, "liboracle.so")
+        # ORACLE_LIB_DIR: the sanitizer build (oracle/_asan, scripts/asan.sh)
+        path = os.path.join(os.environ.get("ORACLE_LIB_DIR") or HERE, "liboracle.so")
         if not os.path.exists(path):
             raise ImportError("oracle/liboracle.so missing: run `make -C oracle`")
         L = C.CDLL(path)

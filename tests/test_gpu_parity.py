@@ -25,6 +25,14 @@ def ctx():
     return D.Context(0)
 
 
+@pytest.fixture(autouse=True)
+def _auto_shape(request):
+    """Every test starts and ends with the automatic kernel shape (bc_ctx_set_shape)."""
+    yield
+    if "ctx" in request.fixturenames:
+        request.getfixturevalue("ctx").set_shape("auto")
+
+
 def gpu_count(ctx, b, L, mbq, ncols, **kw):
     b = dict(b, **kw)
     r = D.DeviceReads(ctx, b)
@@ -92,10 +100,10 @@ def random_batch(rng, L, n, long_skip=False, sort=True, nfrac=0.05):
 ])
 @pytest.mark.parametrize("mbq", [0, 20, 40])
 @pytest.mark.parametrize("path", ["tile", "rc"])
-def test_kernel1_matches_oracle(ctx, monkeypatch, seed, L, n, sort, long_skip, mbq, path):
+def test_kernel1_matches_oracle(ctx, seed, L, n, sort, long_skip, mbq, path):
     """Sorted batches take the tiled (k_pileup) or the read-chunked (k_rc) kernel, unsorted
     ones the event-parallel k_count: identical counts."""
-    monkeypatch.setenv("BC_PILEUP_PATH", path)
+    ctx.set_shape(path)
     rng = np.random.default_rng(seed)
     b = random_batch(rng, L, n, long_skip=long_skip, sort=sort)
     exp, (br, _) = O.bcount(L, mbq, b)
@@ -150,10 +158,10 @@ FALLBACK = [[(2, 3), (0, 147)], [(0, 147), (2, 3)], [(0, 50), (2, 2), (0, 50), (
 
 @pytest.mark.parametrize("mix", ["image", "fallback", "mixed"])
 @pytest.mark.parametrize("mbq,ncols", [(0, 5), (20, 6)])
-def test_rc_event_image_shapes(ctx, monkeypatch, mix, mbq, ncols):
+def test_rc_event_image_shapes(ctx, mix, mbq, ncols):
     """Deep sorted batches through k_rc: chunks the event image takes, chunks whose reads start
     or end with a deletion / have 3 runs / span too many windows (run tables), and both mixed."""
-    monkeypatch.setenv("BC_PILEUP_PATH", "rc")
+    ctx.set_shape("rc")
     tpl = {"image": IMAGE_OK, "fallback": FALLBACK, "mixed": IMAGE_OK + FALLBACK[:2]}[mix]
     rng = np.random.default_rng({"image": 31, "fallback": 32, "mixed": 33}[mix])
     L = 12_000
@@ -165,10 +173,10 @@ def test_rc_event_image_shapes(ctx, monkeypatch, mix, mbq, ncols):
     assert np.array_equal(got, exp[:, :ncols].T.astype(np.int32)), mix
 
 
-def test_rc_event_image_range_error(ctx, monkeypatch):
+def test_rc_event_image_range_error(ctx):
     """A read running past the reference end inside an imaged chunk: the reference's first
     offending read (std::out_of_range), nothing counted past L."""
-    monkeypatch.setenv("BC_PILEUP_PATH", "rc")
+    ctx.set_shape("rc")
     rng = np.random.default_rng(34)
     L = 5_000
     b = shaped_batch(rng, L + 400, 30_000, IMAGE_OK[:4])
@@ -178,26 +186,34 @@ def test_rc_event_image_range_error(ctx, monkeypatch):
     assert bad == br
 
 
-def test_kernel1_rpb_and_window_paths(ctx, monkeypatch):
-    """Same counts whatever the chunking: tiny chunks, huge chunks (global-atomic path)."""
+def test_kernel1_rpb_and_window_paths(ctx):
+    """Same counts whatever the chunking: tiny chunks, huge chunks (global-atomic path), every
+    waves-per-tile of the tiled kernel, with and without the sparse sweep."""
     rng = np.random.default_rng(9)
     b = random_batch(rng, 3_000, 8_000)
     exp, _ = O.bcount(3_000, 0, b)
-    for rpb in ("1", "7", "64", "4096", "30000"):
-        monkeypatch.setenv("BC_RPB", rpb)
-        got, bad = gpu_count(ctx, b, 3_000, 0, 6)
+    perm0 = np.random.default_rng(2).permutation(b["pos"].size)
+    bu0 = dict(b, pos=b["pos"][perm0], cig_beg=b["cig_beg"][perm0], cig_n=b["cig_n"][perm0],
+               seq_nib=b["seq_nib"][perm0])
+    for rpb in (1, 7, 64, 4096, 30000):
+        ctx.set_shape("auto", 0, rpb)
+        got, bad = gpu_count(ctx, bu0, 3_000, 0, 6)
         assert bad == -1 and np.array_equal(got, exp.T.astype(np.int32)), rpb
-    monkeypatch.delenv("BC_RPB")
+    ctx.set_shape("auto")
     # unsorted order takes the event-parallel kernel: same counts
     perm = np.random.default_rng(1).permutation(b["pos"].size)
     bu = dict(b, pos=b["pos"][perm], cig_beg=b["cig_beg"][perm], cig_n=b["cig_n"][perm],
               seq_nib=b["seq_nib"][perm])
     got, bad = gpu_count(ctx, bu, 3_000, 0, 6)
     assert bad == -1 and np.array_equal(got, exp.T.astype(np.int32))
-    for waves in ("1", "2", "4", "8", "16"):
-        monkeypatch.setenv("BC_TILE_WAVES", waves)
-        got, bad = gpu_count(ctx, b, 3_000, 0, 6)
-        assert bad == -1 and np.array_equal(got, exp.T.astype(np.int32)), waves
+    for shape in ("tile", "tile_no_solo"):
+        for waves in (1, 2, 4, 8):
+            ctx.set_shape(shape, waves)
+            got, bad = gpu_count(ctx, b, 3_000, 0, 6)
+            assert bad == -1 and np.array_equal(got, exp.T.astype(np.int32)), (shape, waves)
+    for bad_waves in (3, 5, 6, 7, 16):  # ADVICE r1: must divide the block's waves
+        with pytest.raises(D.BcError):
+            ctx.set_shape("tile", bad_waves)
 
 
 def test_kernel1_range_error_first_read(ctx):
@@ -233,8 +249,8 @@ def gpu_pileup(ctx, b, L, mbq, k):
                                       (14, 2_000_000, 3_000), (15, 64, 50), (16, 65, 80)])
 @pytest.mark.parametrize("mbq,show_n", [(0, False), (20, True), (40, False)])
 @pytest.mark.parametrize("path", ["tile", "rc"])
-def test_fused_pileup_matches_oracle(ctx, monkeypatch, seed, L, n, mbq, show_n, path):
-    monkeypatch.setenv("BC_PILEUP_PATH", path)
+def test_fused_pileup_matches_oracle(ctx, seed, L, n, mbq, show_n, path):
+    ctx.set_shape(path)
     rng = np.random.default_rng(seed)
     b = random_batch(rng, L, n)
     k = 6 if show_n else 5
@@ -249,8 +265,8 @@ def test_fused_pileup_matches_oracle(ctx, monkeypatch, seed, L, n, mbq, show_n, 
 
 
 @pytest.mark.parametrize("path", ["tile", "rc"])
-def test_fused_pileup_range_error(ctx, monkeypatch, path):
-    monkeypatch.setenv("BC_PILEUP_PATH", path)
+def test_fused_pileup_range_error(ctx, path):
+    ctx.set_shape(path)
     rng = np.random.default_rng(21)
     b = random_batch(rng, 2_000, 3_000)
     for L2 in (1_990, 1_900, 1_000, 64):
@@ -419,8 +435,8 @@ def test_bcount_adapter_matches_reference_vectors(golden):
 # ------------------------------------------------------------------ full-size configurations
 @pytest.mark.parametrize("cfg,mmq,mbq", [("c2", 0, 0), ("c3", 0, 0), ("c3", 30, 20)])
 @pytest.mark.parametrize("path", ["tile", "rc"])
-def test_full_size_configs_exact(ctx, monkeypatch, cfg, mmq, mbq, path):
-    monkeypatch.setenv("BC_PILEUP_PATH", path)
+def test_full_size_configs_exact(ctx, cfg, mmq, mbq, path):
+    ctx.set_shape(path)
     rs = synth.make_config(cfg)
     b = synth.batch_arrays(rs, 0, mmq)
     L = rs.lengths[0]
@@ -433,10 +449,9 @@ def test_full_size_configs_exact(ctx, monkeypatch, cfg, mmq, mbq, path):
 
 
 @pytest.mark.parametrize("path", ["auto", "tile", "rc"])
-def test_full_size_c3_fused_pileup(ctx, monkeypatch, path):
+def test_full_size_c3_fused_pileup(ctx, path):
     """The bench's step (bc_pileup) on the full C3 batch: counts exact, stats within 1e-6."""
-    if path != "auto":
-        monkeypatch.setenv("BC_PILEUP_PATH", path)
+    ctx.set_shape(path)
     rs = synth.make_config("c3")
     b = synth.batch_arrays(rs, 0, 0)
     L = rs.lengths[0]

@@ -54,6 +54,8 @@ class BcioRecords(C.Structure):
         ("qual", C.c_void_p),
         ("seq_bytes", C.c_uint64),
         ("ref_span", C.c_void_p),
+        ("seq_event", C.c_void_p),
+        ("seq_event_bytes", C.c_uint64),
     ]
 
 
@@ -114,6 +116,7 @@ def bcio() -> C.CDLL:
     lib.bcio_get_records.argtypes = [C.c_void_p, C.POINTER(BcioRecords)]
     lib.bcio_select.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(BcioSelection)]
     lib.bcio_write_bam.argtypes = [C.c_char_p, C.POINTER(BcioWriteSpec)]
+    lib.bcio_seq_to_event.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int]
     lib.bcio_fmt_new.argtypes = [C.POINTER(C.c_void_p)]
     lib.bcio_fmt_free.argtypes = [C.c_void_p]
     lib.bcio_fmt_free.restype = None

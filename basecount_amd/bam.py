@@ -85,6 +85,8 @@ class BamFile:
         self.seq = _view(r.seq, int(r.seq_bytes), np.uint8)
         self.qual = _view(r.qual, 2 * int(r.seq_bytes), np.uint8)
         self.ref_span = _view(r.ref_span, n, np.int64)
+        # SEQ in the kernels' BC_SEQ_EVENT layout, padded (uploaded as is: no device pass)
+        self.seq_event = _view(r.seq_event, int(r.seq_event_bytes), np.uint8)
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -192,6 +194,20 @@ def write_bam(path, references, lengths, tid, pos, flag, mapq, cig_off, cigar, l
     spec.level = int(level)
     spec.nthreads = int(nthreads)
     N.bcio_check(N.bcio().bcio_write_bam(os.fsencode(path), C.byref(spec)))
+
+
+def seq_event_bytes(nbytes: int) -> int:
+    """Size of the padded BC_SEQ_EVENT buffer for nbytes of BAM-packed SEQ."""
+    return (int(nbytes) + 15) // 16 * 16 + 16
+
+
+def seq_to_event(seq: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """BAM-packed SEQ bytes -> the kernels' BC_SEQ_EVENT layout (padded), on the host."""
+    src = np.ascontiguousarray(seq, np.uint8)
+    out = np.empty(seq_event_bytes(src.size), np.uint8)
+    N.bcio_check(N.bcio().bcio_seq_to_event(src.ctypes.data if src.size else None, src.size,
+                                            out.ctypes.data, out.size, int(nthreads)))
+    return out
 
 
 def pack_seq(seq_str: str) -> np.ndarray:

@@ -144,6 +144,10 @@ int64_t host_bad_pos(const bc_reads& r, int64_t i, int64_t ref_len, uint32_t mbq
 
 }  // namespace
 
+namespace bc {
+int set_error(int code, const std::string& m) { return fail(code, m); }
+}  // namespace bc
+
 extern "C" {
 
 const char* bc_last_error(void) { return g_err.c_str(); }
@@ -307,7 +311,11 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     const auto sp = h->n_reads ? host_spans(*h) : std::pair<int, int64_t>(0, 0);
     d->max_span = sp.first;
     d->max_end = sp.second;
-    if (h->seq_layout != BC_SEQ_BAM) return fail(BC_E_ARG, "bc_reads_upload: host batch must be BC_SEQ_BAM");
+    if (h->seq_layout != BC_SEQ_BAM && h->seq_layout != BC_SEQ_EVENT)
+        return fail(BC_E_ARG, "bc_reads_upload: unknown seq_layout");
+    // BC_SEQ_EVENT from the host (the decoder's bcio_records.seq_event): a plain copy, no device
+    // conversion pass; BC_SEQ_BAM is converted in place by k_seq_event after the copy
+    const bool host_event = h->seq_layout == BC_SEQ_EVENT;
     const size_t n = (size_t)h->n_reads;
     void* p[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // the sequence buffer is sized for BC_SEQ_EVENT (converted in place after the copy)
@@ -331,7 +339,12 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
         if (!sz[i]) continue;
         p[i] = (uint8_t*)slab + off[i];
         hipError_t e = cp[i] ? hipMemcpyAsync(p[i], src[i], cp[i], hipMemcpyHostToDevice, c->stream) : hipSuccess;
-        if (e == hipSuccess && i == 5) e = bc::launch_seq_event(c->stream, (const uint8_t*)p[5], h->seq_bytes, (uint8_t*)p[5]);
+        if (e == hipSuccess && i == 5) {
+            if (host_event)  // zero padding past the copied bytes
+                e = hipMemsetAsync((uint8_t*)p[5] + cp[5], 0, sz[5] - cp[5], c->stream);
+            else
+                e = bc::launch_seq_event(c->stream, (const uint8_t*)p[5], h->seq_bytes, (uint8_t*)p[5]);
+        }
         if (e != hipSuccess) {
             (void)hipStreamSynchronize(c->stream);
             (void)hipFree(slab);
@@ -581,6 +594,7 @@ int bc_bcount_host(int device, int64_t ref_len, uint32_t mbq, const bc_reads* h,
     int rc = check_host_reads(h);
     if (rc) return rc;
     if (mbq > 0 && h->n_reads > 0 && !h->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+    if (h->seq_layout != BC_SEQ_BAM) return fail(BC_E_ARG, "bc_bcount_host takes BC_SEQ_BAM sequences");
     bc_ctx* c = nullptr;
     rc = bc_ctx_create(device, nullptr, &c);
     if (rc) return rc;

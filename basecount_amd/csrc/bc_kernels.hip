@@ -9,6 +9,7 @@
 // Integer scatter, not a contraction: no MFMA.  Kernel 1 is bound by HBM (read records) and by
 // the LDS atomic rate; see DESIGN.md for the roofline accounting.
 #include "bc_internal.h"
+#include "bc_log2.h"
 
 namespace bc {
 namespace {
@@ -292,11 +293,11 @@ __global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, in
         if (in && cov != 0) {
             const double pj = (double)cj / (double)cov;
             if (pc) pc[(int64_t)j * L + p] = 100.0 * pj;
-            if (cj != 0) e1 = -(pj * log2(pj));
+            if (cj != 0) e1 = -(pj * glibc_log2(pj));
             const int64_t cov2 = cov - c[am];
             if (sec && j != am && cj != 0 && cov2 != 0) {
                 const double q = (double)cj / (double)cov2;
-                e2 = -(q * log2(q));
+                e2 = -(q * glibc_log2(q));
             }
         } else if (in && pc) {
             pc[(int64_t)j * L + p] = -1.0;

@@ -21,6 +21,7 @@
 #include <cstring>
 
 #include "bc_internal.h"
+#include "bc_log2.h"
 
 namespace bc {
 namespace {
@@ -203,7 +204,7 @@ __device__ __attribute__((noinline)) void tile_terms(const PileArgs& A, const ui
                 if (c[sc] != 0) {
                     const double pj = (double)c[sc] / (double)cov;
                     if (A.pc) A.pc[(int64_t)sc * L + Pp] = 100.0 * pj;
-                    term = -(pj * log2(pj));
+                    term = -(pj * glibc_log2(pj));
                 } else if (A.pc) {
                     A.pc[(int64_t)sc * L + Pp] = 0.0;  // 100 * (0 / cov), exactly
                 }
@@ -215,7 +216,7 @@ __device__ __attribute__((noinline)) void tile_terms(const PileArgs& A, const ui
             const int64_t cov2 = cov - c[am];
             if (cov2 != 0 && j != am && c[j] != 0) {
                 const double q = (double)c[j] / (double)cov2;
-                term = -(q * log2(q));
+                term = -(q * glibc_log2(q));
             }
         }
         terms_g[sc * kTile + p] = term;
@@ -671,7 +672,7 @@ __device__ __forceinline__ void pos_stats(const PileArgs& A, const uint32_t* c, 
         for (int j = 0; j < K; ++j) {
             const double pj = (double)c[j] / (double)cov;
             if (A.pc) A.pc[(int64_t)j * L + P] = 100.0 * pj;
-            if (c[j] != 0) s = s + (-(pj * log2(pj)));
+            if (c[j] != 0) s = s + (-(pj * glibc_log2(pj)));
         }
         h = A.nf * s;
         const int64_t cov2 = cov - c[am];
@@ -681,7 +682,7 @@ __device__ __forceinline__ void pos_stats(const PileArgs& A, const uint32_t* c, 
             for (int j = 0; j < K; ++j)
                 if (j != am && c[j] != 0) {
                     const double q = (double)c[j] / (double)cov2;
-                    s2 = s2 + (-(q * log2(q)));
+                    s2 = s2 + (-(q * glibc_log2(q)));
                 }
             h2 = A.nf2 * s2;
         }

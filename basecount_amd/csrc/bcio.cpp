@@ -202,6 +202,7 @@ struct bcio_file {
     uvec<uint64_t> cig_off, seq_off;
     uvec<uint32_t> cigar;
     uvec<uint8_t> seq, qual;
+    uvec<uint8_t> seq_ev;  // the same bases in the kernels' BC_SEQ_EVENT layout (+ zero pad)
     // selection outputs: one block per bcio_select call, alive until bcio_close
     struct Sel {
         std::vector<int64_t> ref_beg;
@@ -281,6 +282,26 @@ const Deflate& libdeflate() {
     static const Deflate d;
     return d;
 }
+
+// BAM 4-bit code -> BC_SEQ_EVENT class (basecount_hip.h): A 1, C 2, G 4, T 8, N 3, others 0
+// ('=' and IUPAC codes count nowhere, count.cpp:58-65 through pysam's decode).  A BAM byte holds
+// base 2m in its high nibble; the event layout keeps base i at bits 4*(i%8) of little-endian
+// word i/8, i.e. base 2m in the LOW nibble of byte m: swap and classify, one table lookup.
+struct EventLut {
+    uint8_t t[256];
+    EventLut() {
+        static const uint8_t cls[16] = {0, 1, 2, 0, 4, 0, 0, 0, 8, 0, 0, 0, 0, 0, 0, 3};
+        for (int b = 0; b < 256; ++b) t[b] = (uint8_t)(cls[b >> 4] | (cls[b & 15] << 4));
+    }
+};
+const EventLut kEventLut;
+
+inline void seq_to_event(const uint8_t* src, uint64_t n, uint8_t* dst) {
+    for (uint64_t j = 0; j < n; ++j) dst[j] = kEventLut.t[src[j]];
+}
+
+// bytes of a BC_SEQ_EVENT buffer for n packed bytes (= bc_seq_event_bytes of basecount_hip.h)
+inline uint64_t seq_event_bytes(uint64_t n) { return (n + 15) / 16 * 16 + 16; }
 
 struct Block {
     uint64_t coff, clen, uoff;
@@ -466,6 +487,8 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
     f->rec_err.resize(n);
     f->cigar.resize(cig_tot);
     f->seq.resize(seq_tot);
+    f->seq_ev.resize(seq_event_bytes(seq_tot));
+    std::memset(f->seq_ev.data() + seq_tot, 0, f->seq_ev.size() - seq_tot);
     f->qual.resize(2 * seq_tot);
     pt.mark("starts");
     std::atomic<int> ferr{0};
@@ -500,6 +523,7 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
             const uint8_t* s = c + 4ull * nc;
             uint64_t sb = (((uint64_t)ls + 1) / 2);
             std::memcpy(f->seq.data() + f->seq_off[i], s, sb);
+            seq_to_event(s, sb, f->seq_ev.data() + f->seq_off[i]);
             const uint8_t* ql = s + sb;
             uint8_t* qd = f->qual.data() + 2 * f->seq_off[i];
             std::memcpy(qd, ql, (size_t)ls);
@@ -559,6 +583,8 @@ extern "C" int bcio_get_records(const bcio_file* f, bcio_records* o) {
     o->qual = f->qual.data();
     o->seq_bytes = f->seq_off.empty() ? 0 : f->seq_off.back();
     o->ref_span = f->ref_span.data();
+    o->seq_event = f->seq_ev.data();
+    o->seq_event_bytes = (uint64_t)f->seq_ev.size();
     return BCIO_OK;
 }
 
@@ -1036,5 +1062,18 @@ extern "C" int bcio_fmt_rows(bcio_fmt* b, const char* ref, int64_t L, int k, con
     for (auto& s : parts) tot += s.size();
     b->buf.reserve(tot);
     for (auto& s : parts) b->buf.append(s.data(), s.size());
+    return BCIO_OK;
+}
+
+extern "C" int bcio_seq_to_event(const uint8_t* bam, int64_t nbytes, uint8_t* out, int64_t out_bytes, int nthreads) {
+    if (nbytes < 0 || (nbytes > 0 && (!bam || !out))) return fail(BCIO_E_ARG, "null argument");
+    if ((uint64_t)out_bytes < seq_event_bytes((uint64_t)nbytes))
+        return fail(BCIO_E_ARG, "out_bytes smaller than the padded event layout");
+    const int64_t chunk = 1 << 20;
+    parallel_for((nbytes + chunk - 1) / chunk, hw_threads(nthreads), [&](int64_t c0, int64_t c1) {
+        const int64_t a = c0 * chunk, b = std::min(nbytes, c1 * chunk);
+        seq_to_event(bam + a, (uint64_t)(b - a), out + a);
+    });
+    std::memset(out + nbytes, 0, (size_t)(out_bytes - nbytes));
     return BCIO_OK;
 }

@@ -14,7 +14,8 @@ import numpy as np
 
 from ._native import _libs, _load
 
-BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV = -1, -2, -3, -4
+BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV, BC_E_COMM = -1, -2, -3, -4, -5
+COMM_ID_BYTES = 128  # BC_COMM_ID_BYTES
 BC_SEQ_BAM, BC_SEQ_EVENT = 0, 1
 SHAPES = {"auto": 0, "tile": 1, "rc": 2, "tile_no_solo": 3}  # BC_SHAPE_*
 KERNEL_NAMES = ("count", "stats", "rc", "pileup", "summary", "amplicons")  # BC_K_* ids
@@ -91,6 +92,17 @@ def lib() -> C.CDLL:
         "bc_timing_report": ([vp, vp, vp], C.c_int),
         "bc_event_record": ([vp, C.c_int], C.c_int),
         "bc_event_elapsed_ms": ([vp, C.c_int, C.c_int, C.POINTER(C.c_float)], C.c_int),
+        # multi-GPU (bc_comm.hip)
+        "bc_comm_unique_id": ([vp], C.c_int),
+        "bc_comm_init": ([vp, vp, C.c_int, C.c_int, C.POINTER(vp)], C.c_int),
+        "bc_comm_destroy": ([vp], C.c_int),
+        "bc_comm_rank": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
+        "bc_comm_barrier": ([vp], C.c_int),
+        "bc_allgather_i64": ([vp, vp, i64, vp], C.c_int),
+        "bc_broadcast_bytes": ([vp, vp, i64, C.c_int], C.c_int),
+        "bc_gather_layout": ([vp, C.c_int, vp], C.c_int),
+        "bc_gather_bytes": ([vp, vp, i64, vp, vp, C.c_int], C.c_int),
+        "bc_gather_dev": ([vp, vp, i64, vp, vp, C.c_int], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -174,6 +186,12 @@ def host_reads(b: dict) -> tuple:
         r.qual_bytes = keep["qual"].size
     r.sorted = int(b.get("sorted", 0))
     r.max_span = int(b.get("max_span", 0))
+    if b.get("seq_event") is not None:
+        # the host already holds the kernels' layout (bcio decoder / bam.seq_to_event): sent as
+        # is, no device conversion pass
+        keep["seq"] = np.ascontiguousarray(b["seq_event"], np.uint8)
+        r.seq = keep["seq"].ctypes.data
+        r.seq_layout = BC_SEQ_EVENT
     return r, keep
 
 

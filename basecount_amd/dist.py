@@ -1,22 +1,38 @@
-"""Multi-GPU (one process per GPU) plumbing for the CLI: contig sharding + gather to rank 0.
+"""Multi-GPU (one process per GPU) plumbing for the CLI and the bench: contig sharding, the
+reference order every rank follows, and the gather to rank 0.
 
 The counting path needs no communication: references are independent, so each
 rank owns whole references (LPT on an estimate of their cost) and runs the single-GPU path on
 them.  The only exchanges are
-  * the per-reference range-error indices (all ranks must raise the same first error, in the
-    reference's order: main.py's error timeline), and
-  * the output: summary text is gathered to rank 0 over the process group (RCCL with the
-    "nccl" backend, GPU-resident byte tensors), per-position rows are written by their owner in
-    reference order (barrier per reference), so hundreds of GB of TSV never travel.
+  * the reference order: main.py:92 iterates ``set(references)``, whose order depends on each
+    process's hash seed, so rank 0's order is broadcast and every rank follows it (sharding,
+    error exchange, output order);
+  * the per-reference first out-of-range read (all ranks raise the same first error, in the
+    reference's order: main.py's error timeline);
+  * the output: summary numbers are gathered to rank 0; per-position rows are written by their
+    owner in reference order (barrier per reference), so hundreds of GB of TSV never travel.
+
+Two interchangeable groups implement these exchanges:
+  * ``RcclGroup`` (the product's, default): RCCL over xGMI through the C-ABI of
+    libbasecount_hip.so (bc_comm_*, bc_allgather_i64, bc_broadcast_bytes, bc_gather_bytes), on
+    the rank's own GPU and stream.  No PyTorch anywhere: one HIP runtime per process.  The RCCL
+    unique id is handed from rank 0 to the others over a TCP socket at MASTER_ADDR, port
+    ``BASECOUNT_RDZV_PORT`` (default MASTER_PORT + 1: torchrun's own store holds MASTER_PORT).
+  * ``GlooGroup``: torch.distributed's gloo backend on the CPU (``BASECOUNT_DIST_BACKEND=gloo``),
+    for multi-process tests without one GPU per rank (RCCL refuses two ranks on one GPU).
 
 Launch: ``python -m torch.distributed.run --nproc-per-node N -m basecount_amd BAM ...`` (each
-rank reads RANK / LOCAL_RANK / WORLD_SIZE; MASTER_ADDR=127.0.0.1).  Torch's bundled HIP runtime
-must initialise before libbasecount_hip's, so ``init()`` runs first in ``run()``.
+rank reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT).
 """
 from __future__ import annotations
 
+import ctypes as C
+import json
 import os
+import socket
+import struct
 import sys
+import time
 
 
 def env() -> tuple[int, int, int]:
@@ -25,63 +41,232 @@ def env() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-class Group:
-    """A torch.distributed process group plus the device its byte tensors live on."""
+def Group(backend: str | None = None, ctx=None):
+    """The process group of this job: RCCL (default) or gloo (BASECOUNT_DIST_BACKEND)."""
+    backend = backend or os.environ.get("BASECOUNT_DIST_BACKEND") or "rccl"
+    if backend in ("rccl", "nccl"):
+        return RcclGroup(ctx)
+    if backend == "gloo":
+        return GlooGroup()
+    raise ValueError(f"unknown BASECOUNT_DIST_BACKEND {backend!r} (rccl or gloo)")
 
-    def __init__(self, backend: str | None = None):
+
+class _GroupOps:
+    """Operations built on the three primitives every group provides: all_gather_ints,
+    broadcast_bytes and gather_bytes."""
+
+    def broadcast_obj(self, obj):
+        """Rank 0's JSON-serialisable object on every rank."""
+        data = json.dumps(obj).encode() if self.rank == 0 else b""
+        return json.loads(self.broadcast_bytes(data).decode())
+
+
+def agree_order(group, order: list) -> list:
+    """The reference order of rank 0 on every rank (main.py:92's set order is per process)."""
+    mine = list(order)
+    theirs = group.broadcast_obj(mine)
+    if sorted(theirs) != sorted(mine):
+        raise RuntimeError("ranks disagree on the set of references")
+    return theirs
+
+
+class _stdout_to_stderr:
+    """fd-level redirect of stdout to stderr (native libraries write to fd 1 directly)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+def _rdzv_port() -> int:
+    v = os.environ.get("BASECOUNT_RDZV_PORT")
+    if v:
+        return int(v)
+    return int(os.environ.get("MASTER_PORT", "29500")) + 1
+
+
+def _recv_exact(s: socket.socket, n: int) -> bytes:
+    buf = b""
+    while len(buf) < n:
+        part = s.recv(n - len(buf))
+        if not part:
+            raise ConnectionError("rendezvous peer closed the connection")
+        buf += part
+    return buf
+
+
+def rendezvous_id(rank: int, world: int, make_id, timeout: float = 300.0) -> bytes:
+    """Rank 0 calls make_id() and sends the bytes to every other rank over TCP."""
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = _rdzv_port()
+    deadline = time.monotonic() + timeout
+    if rank == 0:
+        uid = make_id()
+        if world == 1:
+            return uid
+        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        srv.bind((addr, port))
+        srv.listen(max(1, world))
+        srv.settimeout(timeout)
+        try:
+            for _ in range(world - 1):
+                conn, _ = srv.accept()
+                with conn:
+                    _recv_exact(conn, 4)  # the peer's rank (kept for debugging)
+                    conn.sendall(struct.pack("<I", len(uid)) + uid)
+        finally:
+            srv.close()
+        return uid
+    while True:
+        try:
+            with socket.create_connection((addr, port), timeout=10) as s:
+                s.sendall(struct.pack("<I", rank))
+                (n,) = struct.unpack("<I", _recv_exact(s, 4))
+                return _recv_exact(s, n)
+        except (ConnectionRefusedError, socket.timeout, OSError):
+            if time.monotonic() > deadline:
+                raise
+            time.sleep(0.05)
+
+
+class RcclGroup(_GroupOps):
+    """RCCL over xGMI through libbasecount_hip.so's bc_comm (one GPU per rank)."""
+
+    backend = "rccl"
+
+    def __init__(self, ctx=None):
+        from . import device as D
+
+        self.D = D
+        world, rank, _ = env()
+        if ctx is None:
+            from .main import context
+
+            ctx = context()
+        self.ctx = ctx
+        L = D.lib()
+
+        def make_id():
+            buf = (C.c_uint8 * D.COMM_ID_BYTES)()
+            D.check(L.bc_comm_unique_id(buf))
+            return bytes(buf)
+
+        uid = rendezvous_id(rank, world, make_id)
+        h = C.c_void_p()
+        ubuf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+        self.world, self.rank = world, rank
+        # RCCL prints a version banner on fd 1 when a communicator comes up: keep stdout for the
+        # TSV output (the first collective runs inside the redirect too)
+        with _stdout_to_stderr():
+            D.check(L.bc_comm_init(ctx.h, ubuf, rank, world, C.byref(h)))
+            self.h = h.value
+            self.barrier()
+
+    def barrier(self):
+        self.D.check(self.D.lib().bc_comm_barrier(self.h))
+
+    def all_gather_ints(self, vals: list[int]) -> list[list[int]]:
+        import numpy as np
+
+        a = np.ascontiguousarray(vals, np.int64)
+        out = np.zeros(self.world * a.size, np.int64)
+        self.D.check(self.D.lib().bc_allgather_i64(self.h, a.ctypes.data, a.size, out.ctypes.data))
+        return out.reshape(self.world, a.size).tolist()
+
+    def broadcast_bytes(self, data: bytes) -> bytes:
+        n = self.all_gather_ints([len(data)])[0][0]
+        buf = (C.c_uint8 * max(1, n))()
+        if self.rank == 0 and n:
+            C.memmove(buf, data, n)
+        self.D.check(self.D.lib().bc_broadcast_bytes(self.h, buf, n, 0))
+        return bytes(buf)[:n]
+
+    def gather_bytes(self, data: bytes) -> list[bytes] | None:
+        """Rank 0 receives every rank's bytes (ragged sizes, bc_gather_layout offsets)."""
+        import numpy as np
+
+        sizes = np.ascontiguousarray([s[0] for s in self.all_gather_ints([len(data)])], np.int64)
+        offs = gather_layout(sizes)
+        src = (C.c_uint8 * max(1, len(data)))()
+        if data:
+            C.memmove(src, data, len(data))
+        dst = (C.c_uint8 * max(1, int(offs[-1])))() if self.rank == 0 else None
+        self.D.check(self.D.lib().bc_gather_bytes(self.h, src, len(data), dst, sizes.ctypes.data, 0))
+        if self.rank != 0:
+            return None
+        raw = bytes(dst)
+        return [raw[offs[r]: offs[r + 1]] for r in range(self.world)]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.D.lib().bc_comm_destroy(self.h)
+            self.h = None
+
+
+def gather_layout(sizes) -> list[int]:
+    """bc_gather_layout: offsets [world + 1] of a ragged gather (host arithmetic, no GPU)."""
+    import numpy as np
+
+    from . import device as D
+
+    s = np.ascontiguousarray(sizes, np.int64)
+    out = np.zeros(s.size + 1, np.int64)
+    D.check(D.lib().bc_gather_layout(s.ctypes.data, int(s.size), out.ctypes.data))
+    return out.tolist()
+
+
+class GlooGroup(_GroupOps):
+    """torch.distributed gloo on the CPU: multi-process tests without one GPU per rank."""
+
+    backend = "gloo"
+
+    def __init__(self):
         import torch
         import torch.distributed as td
 
         self.td, self.torch = td, torch
-        world, rank, local = env()
-        if backend is None:
-            backend = os.environ.get("BASECOUNT_DIST_BACKEND") or (
-                "nccl" if torch.cuda.is_available() else "gloo")
-        self.backend = backend
-        if backend == "nccl":
-            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-            self.dev = torch.device("cuda", torch.cuda.current_device())
-        else:
-            self.dev = torch.device("cpu")
         if not td.is_initialized():
-            kw = {"device_id": self.dev} if backend == "nccl" else {}
-            # the backends log connection messages on fd 1: keep stdout for the TSV output
-            sys.stdout.flush()
-            saved = os.dup(1)
-            try:
-                os.dup2(2, 1)
-                td.init_process_group(backend, **kw)
-            finally:
-                os.dup2(saved, 1)
-                os.close(saved)
+            # the backend logs connection messages on fd 1: keep stdout for the TSV output
+            with _stdout_to_stderr():
+                td.init_process_group("gloo")
         self.world, self.rank = td.get_world_size(), td.get_rank()
 
     def barrier(self):
-        if self.backend == "nccl":
-            self.td.barrier(device_ids=[self.dev.index])
-        else:
-            self.td.barrier()
+        self.td.barrier()
 
     def all_gather_ints(self, vals: list[int]) -> list[list[int]]:
-        """Every rank's list of int64 (same length on all ranks)."""
-        t = self.torch.tensor(vals, dtype=self.torch.int64, device=self.dev)
+        t = self.torch.tensor(vals, dtype=self.torch.int64)
         out = [self.torch.empty_like(t) for _ in range(self.world)]
         self.td.all_gather(out, t)
-        return [o.cpu().tolist() for o in out]
+        return [o.tolist() for o in out]
+
+    def broadcast_bytes(self, data: bytes) -> bytes:
+        n = self.all_gather_ints([len(data)])[0][0]
+        buf = self.torch.zeros(max(1, n), dtype=self.torch.uint8)
+        if self.rank == 0 and n:
+            buf[:n] = self.torch.frombuffer(bytearray(data), dtype=self.torch.uint8)
+        self.td.broadcast(buf, 0)
+        return bytes(buf.numpy()[:n])
 
     def gather_bytes(self, data: bytes) -> list[bytes] | None:
-        """Rank 0 receives every rank's bytes (ragged: sizes first, then padded payloads)."""
         sizes = [s[0] for s in self.all_gather_ints([len(data)])]
+        offs = gather_layout(sizes)
         n = max(sizes) if sizes else 0
         buf = self.torch.zeros(max(1, n), dtype=self.torch.uint8)
         if data:
             buf[: len(data)] = self.torch.frombuffer(bytearray(data), dtype=self.torch.uint8)
-        buf = buf.to(self.dev)
         outs = [self.torch.empty_like(buf) for _ in range(self.world)]
         self.td.all_gather(outs, buf)
         if self.rank != 0:
             return None
-        return [bytes(o.cpu().numpy()[: sizes[i]]) for i, o in enumerate(outs)]
+        assert offs[-1] == sum(sizes)
+        return [bytes(o.numpy()[: sizes[i]]) for i, o in enumerate(outs)]
 
     def close(self):
         if self.td.is_initialized():
@@ -105,9 +290,10 @@ def _stdout_bytes(data: bytes) -> None:
     sys.stdout.buffer.flush()
 
 
-def ordered_write(group: Group, order: list[str], owner: dict, blocks: dict, write=None) -> None:
-    """Write each reference's bytes in `order`, by its owning rank, one reference at a time
-    (all ranks share the launcher's stdout; the barrier after each reference keeps the order)."""
+def ordered_write(group, order: list[str], owner: dict, blocks: dict, write=None) -> None:
+    """Write each reference's bytes in `order` (rank 0's, agree_order), by its owning rank, one
+    reference at a time (all ranks share the launcher's stdout; the barrier after each reference
+    keeps the order)."""
     write = write or _stdout_bytes
     for ref in order:
         if owner[ref] == group.rank and ref in blocks:

@@ -329,9 +329,10 @@ class _FileOnDevice:
         # reference spans per read (for the LDS window bound), from the decoder
         self.span = np.where(faulty, 0, sel.span)
         self.d_cigar = ctx.alloc(max(4, f.cigar.nbytes)).upload(f.cigar)
-        # packed SEQ in the kernels' layout (BC_SEQ_EVENT), converted in place on the device
-        self.d_seq = ctx.alloc(D.seq_event_bytes(f.seq.nbytes)).upload(f.seq)
-        ctx.seq_to_event(self.d_seq.ptr, f.seq.nbytes, self.d_seq.ptr)
+        # packed SEQ in the kernels' layout (BC_SEQ_EVENT, padded): the decoder built it while
+        # filling the records, so the upload is a plain copy (no device conversion pass)
+        assert f.seq_event.size == D.seq_event_bytes(f.seq.nbytes)
+        self.d_seq = ctx.alloc(f.seq_event.size).upload(f.seq_event)
         self.d_qual = ctx.alloc(max(4, f.qual.nbytes)).upload(f.qual) if need_qual else None
         self.n_cig, self.n_seq, self.n_qual = f.cigar.size, f.seq.size, f.qual.size
         m = sel.pos.size
@@ -380,6 +381,11 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
         ref_index = {n: i for i, n in enumerate(names)}
         reference_lengths = {ref: samfile.lengths[names.index(ref)] for ref in references}
         ref_order = list(references)
+        if _group is not None:
+            from .dist import agree_order
+
+            # main.py:92's set order is per process (hash seed): every rank follows rank 0's
+            ref_order = agree_order(_group, ref_order)
         sel = samfile.select(min_mapping_quality, [n in references for n in names])
         mbq = int(min_base_quality)
         k = 6 if show_n_bases else 5
@@ -671,7 +677,7 @@ def run(argv=None):
                                     provided_once=True))
     from . import dist
 
-    group = dist.Group() if dist.env()[0] > 1 else None  # before the HIP library
+    group = dist.Group() if dist.env()[0] > 1 else None  # RCCL (default) or gloo, DESIGN.md §6
     try:
         _run(args, references, min_base_quality, min_mapping_quality, chunk_size, bed,
              decimal_places, group)

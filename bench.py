@@ -1,27 +1,37 @@
 """Benchmark: reference positions/sec of the pileup hot path on MI355X.
 
-A step = one pass of the hot path over one batch already resident in HBM: ONE launch of the
-fused k_pileup kernel = kernel 1 (CIGAR-expand + base counting, count.cpp:22-97) and kernel 2
-(per-position coverage / percentages / entropies, main.py:29-78).  Workload at N=1: BASELINE config 2 (1 contig 29,903 bp, 100,000 reads x 150 bp,
-all-M CIGAR).  At N>1 every rank runs its own contig of that shape (contig sharding, weak
-scaling, no collective inside the step); the per-contig results are gathered to rank 0 over
-RCCL once after the timed region (reported as gather_ms).
+A step = one pass of the hot path over one batch already resident in HBM: kernel 1 (CIGAR-expand
++ base counting, count.cpp:22-97) and kernel 2 (per-position coverage / percentages /
+entropies, main.py:29-78), for every contig the rank owns.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5] [--launch graph|eager]
 
-The K timed steps are captured into one hipGraph and launched once (default; --launch eager
-issues them one by one): the same kernels on the same data, without the per-launch host and
-command-processor gaps that a ~15 us step otherwise pays.
+Headline (``value``): BASELINE config 2 (1 contig 29,903 bp, 100,000 reads x 150 bp, all-M CIGAR),
+one launch of the fused k_pileup per step, the K timed steps replayed from one hipGraph
+(``--launch eager`` issues them one by one).  At N>1 every rank runs its own contig of that
+shape (contigs are independent: weak scaling, no collective inside the step); the per-contig
+summaries are gathered to rank 0 over RCCL once after the timed region (``gather_ms``).
 
-C5 (24 human-chromosome-sized contigs, 3.09 Gb, 1.2 M reads) is summary-shaped: the per-position
-percentages are not stored (main.py's --summarise never prints them).
+``extra`` carries the other BASELINE shapes, each timed the same way with its own roofline:
+  * c3 (N=1): 1,000,000 mixed-CIGAR reads on the same contig (deep: k_rc + k_stats);
+  * c5 (every N): 24 GRCh38-sized contigs (3.09 Gb) x 50,000 reads, sharded over the ranks (LPT,
+    strong scaling), summary-shaped (main.py:469-499: no per-position percentages), each step
+    ending with the RCCL gather of every contig's summary to rank 0 (``gather_us``).
+At N=1 rank 0 also times the reference's CPU path (its own compiled count.cpp + get_stats, one
+core), the all-cores C restatement (``cpu_baseline_all_cores``), and the CLI end to end on the C2
+BAM (decode, upload, kernels, formatting: ``e2e``).
+
+Multi-GPU runs use the library's own RCCL communicator (basecount_amd/dist.py, no PyTorch);
+BASECOUNT_DIST_BACKEND=gloo lets several ranks share one GPU for rehearsals.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -37,8 +47,10 @@ WORKLOADS = {
     "c2": "C2: 1 contig 29,903 bp, 100,000 reads x 150 bp, all-M CIGAR (per rank)",
     "c3": "C3: 1 contig 29,903 bp, 1,000,000 reads x 150 bp, mixed M/I/D/=/X/S CIGAR (per rank)",
     "c5": "C5: 24 contigs with GRCh38 chr1-22,X,Y lengths (3.09 Gb), 50,000 reads x 150 bp each, "
-          "all-M CIGAR; contigs sharded over the ranks",
+          "all-M CIGAR; contigs sharded over the ranks, summary + RCCL gather to rank 0 per step",
 }
+KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "rc": "k_rc (read-chunked kernel 1)",
+                "stats": "k_stats (kernel 2)", "summary": "k_sum_chunks + k_sum_final (summary)"}
 
 
 def read_bytes(b: dict, mbq: int, l_seq: np.ndarray) -> int:
@@ -59,10 +71,39 @@ def kernel_bytes(kernel: str, rb: int, L: int, k: int, with_pc: bool = True) -> 
     return {"pileup": rb + 4 * k * L + stats_out, "rc": rb + 4 * k * L, "stats": 4 * k * L + stats_out}[kernel]
 
 
+def host_info() -> dict:
+    model = None
+    with contextlib.suppress(OSError):
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": avail, "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_threads() -> int:
+    """Host threads this job may use: the box's per-job share (OMP_NUM_THREADS), not nproc."""
+    v = os.environ.get("OMP_NUM_THREADS")
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(int(v) if v and v.isdigit() else 16, avail))
+
+
+def _loop(fn, budget_s):
+    done, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            return (time.perf_counter() - t0) / done, done
+
+
 def cpu_baseline(rs, b, L: int, budget_s: float = 10.0) -> dict:
-    """The reference's CPU path on the same workload: its own compiled count.bcount (oracle/_ref,
-    pybind11, Python-list arguments as main.py:146 passes them) + get_stats (main.py:14-79,
-    restated in oracle.get_stats_py).  Single thread, like the reference."""
+    """The reference's CPU path on the full C2 workload: its own compiled count.bcount
+    (oracle/_ref, pybind11, Python-list arguments as main.py:146 passes them) + get_stats
+    (main.py:14-79, restated in oracle.get_stats_py).  Single thread, like the reference."""
     import oracle as O
 
     ref = O.ref_bcount()
@@ -77,153 +118,266 @@ def cpu_baseline(rs, b, L: int, budget_s: float = 10.0) -> dict:
         quals = [q for q in rs.qual.reshape(n, -1).tolist()]
         starts = b["pos"].tolist()
         ctuples = [[(0, 150)]] * n
-        done, t0 = 0, time.perf_counter()
-        while True:
-            counts = ref(L, 0, reads, quals, starts, ctuples)
-            O.get_stats_py(counts, "ref")
-            done += 1
-            if time.perf_counter() - t0 > budget_s:
-                break
-        dt = (time.perf_counter() - t0) / done
+        dt, done = _loop(lambda: O.get_stats_py(ref(L, 0, reads, quals, starts, ctuples), "ref"), budget_s)
         kind, what = "reference", ("reference count.cpp (pybind11 bcount, list arguments) + "
                                    "get_stats main.py:14-79 (Python)")
     else:
-        done, t0 = 0, time.perf_counter()
-        while True:
-            counts, _ = O.bcount(L, 0, b)
-            O.stats(counts, False)
-            done += 1
-            if time.perf_counter() - t0 > budget_s:
-                break
-        dt = (time.perf_counter() - t0) / done
+        dt, done = _loop(lambda: O.stats(O.bcount(L, 0, b)[0], False), budget_s)
         kind, what = "port", "oracle C restatement of bcount + get_stats"
-    return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind,
+    return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind, "host": host_info(),
             "sample": f"{what}; full C2 workload ({n} reads, {L} positions) x {done} runs, "
                       f"{dt * 1e3:.1f} ms per run, BAM decode excluded"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--mbq", type=int, default=0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
-                    help="graph: the K timed steps are captured into ONE hipGraph and launched once")
-    args = ap.parse_args()
+def cpu_baseline_all_cores(b, L: int, budget_s: float = 5.0) -> dict:
+    """the C restatement of count.cpp:22-97 + main.py:14-79 on all the job's
+    host threads (mt_oracle.c: read ranges into private histograms, positions split for the
+    statistics), on the full C2 workload."""
+    import oracle as O
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = torch = None
-    if world > 1:
-        # torch's bundled HIP runtime must initialise before libbasecount_hip's (/opt/rocm) one:
-        # the other order leaves torch without devices ("two HIP runtimes")
-        import torch
-        import torch.distributed as dist
+    T = cpu_threads()
+    dt, done = _loop(lambda: O.stats(O.bcount(L, 0, b, nthreads=T)[0], False, nthreads=T), budget_s)
+    return {"value": L / dt, "unit": "positions/s", "cores": T, "kind": "port",
+            "sample": f"oracle C restatement of bcount + get_stats on {T} threads; full C2 workload "
+                      f"({int(b['pos'].size)} reads, {L} positions) x {done} runs, {dt * 1e3:.2f} ms "
+                      f"per run, BAM decode excluded"}
 
-        # one process per GPU; BASECOUNT_DIST_BACKEND=gloo lets ranks share a GPU (rehearsals)
-        backend = os.environ.get("BASECOUNT_DIST_BACKEND", "nccl")
-        dev = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(dev)
-        sys.stdout.flush()
-        saved = os.dup(1)  # the backends log connection messages on fd 1: rank 0 prints ONE line
-        try:
-            os.dup2(2, 1)
-            if backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-            else:
-                dist.init_process_group(backend)
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
 
-    from basecount_amd import device as D
+def e2e_c2(rs) -> dict:
+    """The CLI end to end on the C2 BAM: host decode (BGZF inflate + records,
+    including the BC_SEQ_EVENT layout), upload, kernels, download and the byte-exact TSV
+    formatter, best of 3 warm runs, output to /dev/null."""
+    from basecount_amd import fmt
+    from basecount_amd import main as M
     from basecount_amd import synth
-    from basecount_amd.main import norm_factors
+    from basecount_amd.bam import BamFile
 
-    # ---- workload: this rank's contigs -----------------------------------------------------
-    # c2 / c3: one contig of the config's shape per rank (weak scaling); c5: the 24 GRCh38-sized
-    # contigs, sharded over the ranks by LPT (strong scaling: the total work is fixed)
-    c = synth.CONFIGS[args.config]
-    per_contig = c.get("per_contig", False)
-    if per_contig:
+    tmp = tempfile.mkdtemp(prefix="bc_bench_")
+    bam = os.path.join(tmp, "c2.bam")
+    synth.write_bam(rs, bam)
+
+    def best(fn, reps=3):
+        t = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            t = min(t, time.perf_counter() - t0)
+        return t * 1e3
+
+    def decode():
+        with BamFile(bam) as f:
+            f.select(0, [True] * len(f.references))
+
+    def pipeline():
+        data = M.get_basecounts(bam)
+        for ref, v in data.items():
+            d = v["rows"].d
+            fmt.rows_text(ref, d.counts, d.pc, d.ent, d.sec, 3, False)
+
+    def cli():
+        with open(os.devnull, "w") as fh, contextlib.redirect_stdout(fh):
+            M.run([bam])
+
+    out = {"bam_bytes": os.path.getsize(bam), "decode_ms": best(decode),
+           "decode_count_format_ms": best(pipeline), "cli_ms": best(cli)}
+    out["cli_positions_per_s"] = rs.lengths[0] / (out["cli_ms"] * 1e-3)
+    with contextlib.suppress(OSError):
+        os.remove(bam)
+        os.rmdir(tmp)
+    return out
+
+
+class Workload:
+    """One config's contigs for this rank, resident in HBM before anything is timed."""
+
+    def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool):
+        from basecount_amd import device as D
+        from basecount_amd import synth
+        from basecount_amd.bam import seq_to_event
         from basecount_amd.dist import shard
+        from basecount_amd.main import norm_factors
 
-        contigs = list(c["contigs"])
-        owner = shard([n for n, _ in contigs], dict(contigs), world)
-        mine = [(n, L) for n, L in contigs if owner[n] == rank]
-        rs = synth.make_reads(mine, c["reads"], c["mixed"], c["seed"] + 1000 * rank)
-        total_positions = sum(L for _, L in contigs)
-    else:
-        name = "MN908947.3" if world == 1 else f"contig{rank}"
-        rs = synth.make_reads([(name, c["contigs"][0][1])], c["reads"], c["mixed"],
-                              c["seed"] + 1000 * rank)
-        total_positions = world * rs.lengths[0]
-    ncols = k = 5
-    want_pc = not per_contig  # c5 is only ever summarised: no per-position percentages
-    ctx = D.Context(local % max(1, D.device_count()) if world > 1 else 0)  # own stream
-    nf, nf2 = norm_factors(k)
-    work = []  # one entry per contig, resident in HBM before anything is timed
-    for t, L in enumerate(rs.lengths):
-        b = synth.batch_arrays(rs, t, 0)
-        reads = D.DeviceReads(ctx, b)
-        assert reads.r.sorted == 1
-        bufs = dict(counts=ctx.alloc(4 * ncols * L), cov=ctx.alloc(4 * L),
-                    pc=ctx.alloc(8 * k * L) if want_pc else None, ent=ctx.alloc(8 * L), sec=ctx.alloc(8 * L))
-        work.append((t, L, b, reads, bufs))
+        self.D, self.ctx, self.cfg, self.mbq = D, ctx, cfg, mbq
+        c = synth.CONFIGS[cfg]
+        self.per_contig = c.get("per_contig", False)
+        self.mixed = c["mixed"]
+        if self.per_contig:
+            contigs = list(c["contigs"])
+            owner = shard([n for n, _ in contigs], dict(contigs), world)
+            mine = [(n, L) for n, L in contigs if owner[n] == rank]
+            self.rs = synth.make_reads(mine, c["reads"], c["mixed"], c["seed"] + 1000 * rank)
+            self.total_positions = sum(L for _, L in contigs)
+        else:
+            name = "MN908947.3" if world == 1 else f"contig{rank}"
+            self.rs = synth.make_reads([(name, c["contigs"][0][1])], c["reads"], c["mixed"],
+                                       c["seed"] + 1000 * rank)
+            self.total_positions = world * self.rs.lengths[0]
+        self.k = 5
+        self.want_pc = not self.per_contig  # c5 is only ever summarised: no percentages
+        self.summarise = summarise
+        self.nf, self.nf2 = norm_factors(self.k)
+        self.work = []
+        ev = None
+        for t, L in enumerate(self.rs.lengths):
+            b = synth.batch_arrays(self.rs, t, 0)
+            if ev is None:  # the read set's SEQ in the kernels' layout, built once on the host
+                ev = seq_to_event(b["seq"])
+            reads = D.DeviceReads(ctx, dict(b, seq_event=ev))
+            assert reads.r.sorted == 1
+            k = self.k
+            bufs = dict(counts=ctx.alloc(4 * k * L), cov=ctx.alloc(4 * L),
+                        pc=ctx.alloc(8 * k * L) if self.want_pc else None, ent=ctx.alloc(8 * L),
+                        sec=ctx.alloc(8 * L))
+            if summarise:
+                bufs["swork"] = ctx.alloc(D.summary_work_bytes(L))
+            self.work.append((t, L, b, reads, bufs))
+        # every contig's 4 summary doubles, contiguous: the rank's gather payload
+        self.d_sum = ctx.alloc(32 * max(1, len(self.work))) if summarise else None
 
-    def ptr(x):
-        return x.ptr if x is not None else None
+    def step(self):
+        ctx = self.ctx
+        for i, (_, L, _, reads, o) in enumerate(self.work):
+            ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
+                       o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
+            if self.summarise:
+                ctx.summary(o["cov"].ptr, o["ent"].ptr, L, o["swork"].ptr, self.d_sum.ptr + 32 * i)
+
+    def count_only(self):
+        for _, L, _, reads, o in self.work:
+            self.ctx.count(reads, L, self.mbq, self.k, o["counts"].ptr)
+
+    def stats_only(self):
+        for _, L, _, _, o in self.work:
+            self.ctx.stats(o["counts"].ptr, L, self.k, self.nf, self.nf2, o["cov"].ptr,
+                           o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
+
+    def summary_only(self):
+        for i, (_, L, _, _, o) in enumerate(self.work):
+            self.ctx.summary(o["cov"].ptr, o["ent"].ptr, L, o["swork"].ptr, self.d_sum.ptr + 32 * i)
+
+    def parity(self) -> bool:
+        """Counts exact and entropy within 1e-6 against the oracle on the rank's smallest contig;
+        on every contig of an all-M config the coverage sums to the events piled (a checksum of
+        checksums); the summary of every contig equals numpy's mean over the downloaded arrays."""
+        import oracle as O
+        from basecount_amd import synth
+
+        ok = True
+        small = min(self.work, key=lambda w: w[1])
+        for t, L, b, reads, o in self.work:
+            if (t, L) == small[:2]:
+                got = o["counts"].download(np.int32, self.k * L).reshape(self.k, L)
+                # private per-thread histograms cost threads x 24 B per position: thread the
+                # count only where that stays small (the statistics always thread)
+                T = cpu_threads() if 24 * L * cpu_threads() < (2 << 30) else 0
+                exp, _ = O.bcount(L, self.mbq, b, nthreads=T)
+                ok = ok and bool(np.array_equal(got, exp[:, :self.k].T.astype(np.int32)))
+                _, _, oent, _ = O.stats(exp, False, nthreads=cpu_threads())
+                ok = ok and float(np.max(np.abs(o["ent"].download(np.float64, L) - oent))) <= 1e-6
+                del got, exp, oent
+            if self.mbq == 0 and not self.mixed:
+                cov = o["cov"].download(np.int32, L)
+                ok = ok and int(cov.astype(np.int64).sum()) == synth.ref_events(self.rs, t)
+                if self.summarise:
+                    s = self.d_sum.download(np.float64, 4, offset_bytes=32 * t)
+                    ok = ok and s[0] == np.mean(cov) and int(s[2]) == int(np.count_nonzero(cov))
+        return ok
+
+    def summaries(self) -> np.ndarray:
+        return self.d_sum.download(np.float64, 4 * len(self.work)).reshape(-1, 4)
+
+    def bytes_dominant(self, dom: str) -> int:
+        return sum(kernel_bytes(dom, read_bytes(b, self.mbq, self.rs.l_seq[self.rs.tid == t]), L, self.k,
+                                self.want_pc) for t, L, b, _, _ in self.work)
+
+    def events(self) -> int:
+        from basecount_amd import synth
+
+        return synth.ref_events(self.rs)
+
+    def free(self):
+        for _, _, _, reads, o in self.work:
+            reads.free()
+            for v in o.values():
+                if v is not None:
+                    v.free()
+        if self.d_sum is not None:
+            self.d_sum.free()
+        self.work = []
+
+
+def max_over_ranks(group, seconds: float) -> float:
+    if group is None:
+        return seconds
+    return max(v[0] for v in group.all_gather_ints([int(seconds * 1e9)])) * 1e-9
+
+
+def gather_summaries(group, wl) -> tuple:
+    """Device gather (bc_gather_dev) of every rank's contig summaries to rank 0 on the rank's
+    stream; returns (sizes, receive buffer or None)."""
+    D, ctx = wl.D, wl.ctx
+    n = 32 * len(wl.work)
+    sizes = np.ascontiguousarray([s[0] for s in group.all_gather_ints([n])], np.int64)
+    dst = ctx.alloc(max(32, int(sizes.sum()))) if group.rank == 0 else None
+    return sizes, dst
+
+
+def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, warmup: int,
+               launch: str, summarise: bool) -> dict:
+    """Time K steps of one config (the bench contract: W warmup, barrier + sync on both sides,
+    max over ranks) and describe them."""
+    from basecount_amd import device as D
+
+    wl = Workload(ctx, cfg, rank, world, args.mbq, summarise)
+    rccl = group is not None and getattr(group, "backend", "") == "rccl"
+    gather = None
+    if summarise and group is not None:
+        gather = gather_summaries(group, wl)
+
+    def gather_step():
+        sizes, dst = gather
+        if rccl:  # stream-ordered RCCL point-to-point receives at rank 0
+            D.check(D.lib().bc_gather_dev(group.h, wl.d_sum.ptr, int(sizes[rank]),
+                                          dst.ptr if dst is not None else None, sizes.ctypes.data, 0))
+        else:  # gloo rehearsal: host gather of the same bytes
+            group.gather_bytes(wl.summaries().tobytes())
 
     def step():
-        # one pass of the hot path over every contig of this rank: kernel 1 + kernel 2
-        for _, L, _, reads, o in work:
-            ctx.pileup(reads, L, args.mbq, k, nf, nf2, o["counts"].ptr, o["cov"].ptr, ptr(o["pc"]),
-                       o["ent"].ptr, o["sec"].ptr)
+        wl.step()
+        if gather is not None:
+            gather_step()
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     ctx.sync()
-    assert ctx.range_error() == -1
-
-    def barrier():
-        if dist:
-            dist.barrier()
-
-    # ---- timed region: K eager back-to-back steps, bracketed by barrier + device sync; hipEvents
-    # on the library's stream (the stream every launch goes to) around the region give the
-    # on-device time per step ---------------------------------------------------------------
+    if ctx.range_error() != -1:
+        raise RuntimeError(f"{cfg}: out-of-range event in a synthetic batch")
     graph = None
-    if args.launch == "graph":  # the same K steps, replayed from one captured graph
-        graph = ctx.capture(lambda: [step() for _ in range(args.steps)])
+    if launch == "graph" and gather is None:  # the same K steps, replayed from one captured graph
+        graph = ctx.capture(lambda: [step() for _ in range(steps)])
         graph.launch()  # untimed replay (first-launch setup)
         ctx.sync()
-    barrier()
+    if group is not None:
+        group.barrier()
     ctx.sync()
     t0 = time.perf_counter()
     ctx.event_record(0)
     if graph is not None:
         graph.launch()
     else:
-        for _ in range(args.steps):
+        for _ in range(steps):
             step()
     ctx.event_record(1)
     ctx.sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    dev_step = ctx.event_elapsed_ms(0, 1) * 1e-3 / args.steps  # s per step on the device
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if group is not None:
+        group.barrier()
+    elapsed = max_over_ranks(group, time.perf_counter() - t0)
+    dev_step = ctx.event_elapsed_ms(0, 1) * 1e-3 / steps
+    del graph
 
-    # ---- which kernels a step launches (library timing facility, per-launch event pairs) -------
+    # which kernels a step launches (library timing facility, per-launch event pairs)
     ctx.timing(True)
-    step()
+    wl.step()
     launched = sorted(ctx.timing_report())
     ctx.timing(False)
 
@@ -235,124 +389,211 @@ def main():
         ctx.event_record(3)
         return ctx.event_elapsed_ms(2, 3) * 1e-3 / reps
 
-    # per-kernel time per step, each timed as a region of back-to-back launches of that kernel
-    # alone (a one-kernel step: the step region itself)
+    reps = max(3, min(steps, 100))
     kern_s = {}
-    if launched == ["pileup"]:
-        # eager launches: the kernel's own average duration (what rocprofv3's kernel trace
-        # reports); a graph replay hides part of the launch gap and would flatter the roofline
-        kern_s["pileup"] = dev_step if graph is None else region(step, max(3, min(args.steps, 100)))
-    else:  # deep batches: k_rc + k_stats (bc_count on the same batch launches k_rc alone)
-        reps = max(3, min(args.steps, 50))
+    if "pileup" in launched:
+        def pile_only():
+            for _, L, _, reads, o in wl.work:
+                ctx.pileup(reads, L, wl.mbq, wl.k, wl.nf, wl.nf2, o["counts"].ptr, o["cov"].ptr,
+                           o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
+        # eager back-to-back launches: the kernel's own average duration (what rocprofv3's kernel
+        # trace reports); a graph replay hides part of the launch gap and would flatter it
+        kern_s["pileup"] = region(pile_only, reps)
+    if "rc" in launched:  # deep batches: k_rc + k_stats (bc_count on the same batch: k_rc alone)
+        kern_s["rc"] = region(wl.count_only, reps)
+        kern_s["stats"] = region(wl.stats_only, reps)
+    if summarise:
+        kern_s["summary"] = region(wl.summary_only, reps)
+    gather_us = None
+    if gather is not None:
+        if group is not None:
+            group.barrier()
+        gather_us = region(gather_step, reps) * 1e6
+    wl.step()  # restore the step's outputs (count-only regions accumulated into the counts)
+    ctx.sync()
+    dom = max((k for k in kern_s if k != "summary"), key=kern_s.get)
 
-        def count_only():
-            for _, L, _, reads, o in work:
-                ctx.count(reads, L, args.mbq, k, o["counts"].ptr)
-
-        def stats_only():
-            for _, L, _, _, o in work:
-                ctx.stats(o["counts"].ptr, L, k, nf, nf2, o["cov"].ptr, ptr(o["pc"]), o["ent"].ptr,
-                          o["sec"].ptr)
-
-        kern_s["rc"] = region(count_only, reps)
-        kern_s["stats"] = region(stats_only, reps)
-        step()  # restore the step's outputs (the count-only regions accumulated into the counts)
+    parity = wl.parity()
+    if gather is not None and rccl:
+        # what rank 0 received on the device = every rank's summaries sent over the host path
+        gather_step()
         ctx.sync()
-    dom = max(kern_s, key=kern_s.get)
+        host = group.gather_bytes(wl.summaries().tobytes())
+        if rank == 0:
+            got = gather[1].download(np.uint8, int(gather[0].sum())).tobytes()
+            parity = parity and got == b"".join(host)
+    if group is not None:
+        parity = all(v[0] == 1 for v in group.all_gather_ints([int(parity)]))
 
-    # ---- correctness of what was timed (rank-local) -----------------------------------------
-    import oracle as O
-
-    parity = True
-    small = min(work, key=lambda w: w[1])  # full oracle check on the smallest contig
-    for t, L, b, reads, o in work:
-        if (t, L) == small[:2]:
-            got = o["counts"].download(np.int32, ncols * L).reshape(ncols, L)
-            exp, _ = O.bcount(L, args.mbq, b)
-            parity = parity and bool(np.array_equal(got, exp[:, :ncols].T.astype(np.int32)))
-            _, _, oent, _ = O.stats(exp, False)
-            parity = parity and float(np.max(np.abs(o["ent"].download(np.float64, L) - oent))) <= 1e-6
-            del got, exp, oent
-        if args.mbq == 0 and not c["mixed"]:
-            # size-independent check on every contig: all-M reads without N bases put every
-            # reference-consuming event into the coverage (a checksum of checksums)
-            cov_sum = int(o["cov"].download(np.int32, L).astype(np.int64).sum())
-            parity = parity and cov_sum == synth.ref_events(rs, t)
-
-    # ---- gather per-contig coverage to rank 0 over RCCL (output step, outside the timing) ----
-    gather_ms = None
-    if dist and not per_contig:
-        L0, o0 = work[0][1], work[0][4]
-        covt = torch.from_numpy(o0["cov"].download(np.int32, L0))
-        if backend == "nccl":
-            covt = covt.cuda()
-            torch.cuda.synchronize()
-        g0 = time.perf_counter()
-        bufs = [torch.zeros_like(covt) for _ in range(world)]
-        dist.all_gather(bufs, covt)  # per-contig coverage of every rank (RCCL over xGMI)
-        if backend == "nccl":
-            torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
-
-    events = synth.ref_events(rs)
-    ms = elapsed / args.steps * 1e3
-    positions = total_positions * args.steps
-    kbytes = sum(kernel_bytes(dom, read_bytes(b, args.mbq, rs.l_seq[rs.tid == t]), L, k, want_pc)
-                 for t, L, b, _, _ in work)
+    kbytes = wl.bytes_dominant(dom)
     achieved = kbytes / kern_s[dom] / 1e9
-    kernel_names = {"pileup": "k_pileup (fused kernel 1 + 2)", "rc": "k_rc (read-chunked kernel 1)",
-                    "stats": "k_stats (kernel 2)"}
     traffic = None
     pmc = os.path.join(REPO, "profiles", "kernel1_pmc.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and world == 1:
         with open(pmc) as fh:
-            pm = json.load(fh).get(args.config, {})
-        if pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom and world == 1:
+            pm = json.load(fh).get(cfg, {})
+        if pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom:
             traffic = pm.get("hbm_bytes_per_launch")
-    n_reads = sum(int(w[2]["pos"].size) for w in work)
+    res = {
+        "workload": WORKLOADS[cfg],
+        "value": wl.total_positions * steps / elapsed,
+        "unit": "positions/s",
+        "ms_per_step": elapsed / steps * 1e3,
+        "steps": steps, "warmup": warmup,
+        "scaling": "strong" if wl.per_contig else "weak",
+        "gbases_piled_per_s": (1 if wl.per_contig else world) * wl.events() * steps / elapsed / 1e9,
+        "device_us_per_step": dev_step * 1e6,
+        "kernel_us": {KERNEL_NAMES[n]: v * 1e6 for n, v in kern_s.items()},
+        "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per contig per step"
+                    if dom == "pileup" else
+                    "k_rc (kernel 1, into a zeroed scratch) + k_stats (kernel 2, moves the counts out "
+                    "and re-zeroes) per contig per step")
+                   + (", + numpy-exact summary per contig" if summarise else "")
+                   + (", + RCCL gather of the summaries to rank 0" if gather is not None else "")
+                   + (", the K timed steps replayed from one hipGraph" if launch == "graph" and gather is None
+                      else ", eager launches"),
+        "reads_per_rank": int(sum(int(w[2]["pos"].size) for w in wl.work)),
+        "positions_per_rank": int(sum(w[1] for w in wl.work)),
+        "contigs_per_rank": len(wl.work),
+        "parity_vs_oracle": parity,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_NAMES[dom],
+                     "algorithmic_bytes": kbytes},
+    }
+    if gather_us is not None:
+        res["gather_us"] = gather_us
+        res["gather_bytes"] = int(gather[0].sum())
+    res["_wl"] = wl
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--mbq", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-extras", action="store_true", help="headline config only")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
+                    help="graph: the K timed steps are captured into ONE hipGraph and launched once")
+    ap.add_argument("--shape", default="auto", choices=["auto", "tile", "rc", "tile_no_solo"],
+                    help="kernel shape override (bc_ctx_set_shape), recorded in the output")
+    ap.add_argument("--tile-waves", type=int, default=0, help="waves per tile override (0 = auto)")
+    ap.add_argument("--allow-diag", action="store_true",
+                    help="run a diagnostic (BC_DIAG) build; its numbers are marked as such")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from basecount_amd import device as D
+    from basecount_amd.main import context
+
+    build = D.build_info()
+    if "diag=0" not in build and not args.allow_diag:
+        sys.exit(f"bench.py: {build!r} is a diagnostic build (work-skipping switches compiled in); "
+                 "rebuild without DIAG=1, or pass --allow-diag")
+    os.environ.setdefault("BASECOUNT_DEVICE", str(local % max(1, D.device_count())))
+    ctx = context()
+    ctx.set_shape(args.shape, args.tile_waves)
+    group = None
+    if world > 1:
+        from basecount_amd.dist import Group
+
+        group = Group(ctx=ctx)  # RCCL over xGMI (BASECOUNT_DIST_BACKEND=gloo: rehearsal)
+
+    head = run_config(args.config, ctx, group, args, rank, world, args.steps, args.warmup, args.launch,
+                      summarise=(args.config == "c5"))
+    wl = head.pop("_wl")
+    # ---- gather of the per-contig summaries to rank 0 (the output step, after the timed region)
+    gather_ms = None
+    if group is not None and args.config != "c5":
+        payload = []
+        for _, L, _, _, o in wl.work:
+            work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+            ctx.summary(o["cov"].ptr, o["ent"].ptr, L, work.ptr, dout.ptr)
+            payload.append(dout.download(np.float64, 4))
+        data = np.concatenate(payload).tobytes()
+        group.barrier()
+        g0 = time.perf_counter()
+        parts = group.gather_bytes(data)
+        gather_ms = max_over_ranks(group, time.perf_counter() - g0) * 1e3
+        if rank == 0:
+            assert len(parts) == world and parts[0] == data
+    wl.free()
+    del wl
+
+    extra = {}
+    if not args.no_extras:
+        todo = (["c3", "c5"] if world == 1 else ["c5"])
+        for cfg in todo:
+            if cfg == args.config:
+                continue
+            st, wu = (min(args.steps, 200), min(args.warmup, 20)) if cfg != "c5" else (min(args.steps, 10), 2)
+            r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=(cfg == "c5"))
+            r.pop("_wl").free()
+            extra[cfg] = r
+
+    cpu = cpu_all = e2e = None
+    if rank == 0 and world == 1:
+        from basecount_amd import synth
+
+        if not args.no_cpu_baseline and args.config == "c2":
+            rs = synth.make_config("c2")
+            b0 = synth.batch_arrays(rs, 0, 0)
+            cpu = cpu_baseline(rs, b0, rs.lengths[0], args.cpu_budget)
+            cpu_all = cpu_baseline_all_cores(b0, rs.lengths[0], min(5.0, args.cpu_budget))
+        if not args.no_e2e and args.config == "c2":
+            e2e = e2e_c2(synth.make_config("c2"))
 
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline and not per_contig:
-            b0, L0 = work[0][2], work[0][1]
-            cpu = cpu_baseline(rs, b0, L0, args.cpu_budget)
-        value = positions / elapsed
         line = {
             "metric": "reference positions/sec (kernel 1 + kernel 2, inputs resident in HBM)",
-            "value": value,
+            "value": head["value"],
             "unit": "positions/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "strong" if per_contig else "weak",
+            "scaling": head["scaling"],
             "vs_baseline": None,
             "dtype": "int32 counts / f64 stats",
             "data": "synthetic (seeded, BASELINE config shape)",
-            "config": {"workload": WORKLOADS[args.config], "reads_per_rank": n_reads,
-                       "positions_per_rank": int(sum(w[1] for w in work)), "contigs_per_rank": len(work),
-                       "min_base_quality": args.mbq, "percentages_stored": want_pc,
-                       "parallelism": f"contig-sharded x{world}"},
-            "gbases_piled_per_s": (world if not per_contig else 1) * events * args.steps / elapsed / 1e9,
-            "device_us_per_step": dev_step * 1e6,
-            "kernel_us": {kernel_names[n]: v * 1e6 for n, v in kern_s.items()},
-            "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per contig per step"
-                        if dom == "pileup" else "k_rc (kernel 1, into a zeroed scratch) + k_stats (kernel 2, moves the counts out and re-zeroes) per contig per step")
-                       + (", the K timed steps replayed from one hipGraph" if graph is not None else ", eager launches"),
-            "parity_vs_oracle": parity,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel_names[dom], "algorithmic_bytes": kbytes},
+            "config": {"workload": head["workload"], "reads_per_rank": head["reads_per_rank"],
+                       "positions_per_rank": head["positions_per_rank"],
+                       "contigs_per_rank": head["contigs_per_rank"], "min_base_quality": args.mbq,
+                       "percentages_stored": args.config != "c5",
+                       "parallelism": f"contig-sharded x{world}",
+                       "comm": (group.backend if group is not None else None),
+                       "shape": args.shape, "tile_waves": args.tile_waves, "build": build},
+            "gbases_piled_per_s": head["gbases_piled_per_s"],
+            "device_us_per_step": head["device_us_per_step"],
+            "kernel_us": head["kernel_us"],
+            "kernels": head["kernels"],
+            "parity_vs_oracle": head["parity_vs_oracle"],
+            "roofline": head["roofline"],
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
             "gather_ms": gather_ms,
+            "e2e": e2e,
+            "extra": extra,
         }
+        if "gather_us" in head:
+            line["gather_us"] = head["gather_us"]
         if cpu:
-            line["speedup_vs_cpu"] = value / cpu["value"]
+            line["speedup_vs_cpu"] = head["value"] / cpu["value"]
+            line["speedup_vs_cpu_all_cores"] = head["value"] / cpu_all["value"]
         print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
-    if not parity:
+    ok = head["parity_vs_oracle"] and all(r["parity_vs_oracle"] for r in extra.values())
+    if group is not None:
+        group.close()
+    if not ok:
         sys.exit(3)
 
 

@@ -40,6 +40,7 @@ extern "C" {
 #define BC_E_HIP (-2)   /* HIP runtime error                                                     */
 #define BC_E_RANGE (-3) /* a counted event fell outside [0, refLen) (count.cpp:60-65,85 .at())   */
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
+#define BC_E_COMM (-5)  /* RCCL error in a multi-GPU call                                        */
 
 #define BC_ABI_VERSION 3
 
@@ -128,7 +129,9 @@ size_t bc_seq_event_bytes(int64_t seq_bytes);
  * alias d_bam.  Async on the context's stream.                                                */
 int bc_seq_to_event(bc_ctx* ctx, const uint8_t* d_bam, int64_t seq_bytes, uint8_t* d_event);
 
-/* Copy a host batch (BC_SEQ_BAM) to HBM (library-owned, converted to BC_SEQ_EVENT).  `sorted`,
+/* Copy a host batch to HBM (library-owned, BC_SEQ_EVENT on the device).  A BC_SEQ_EVENT host
+ * batch (the layout the host decoder already emits, bcio_records.seq_event) is copied as is; a
+ * BC_SEQ_BAM one is converted on the device after the copy (k_seq_event).  `sorted`,
  * `max_span` and `max_end` of the device batch are derived from the data (the host's values
  * are ignored).  For batches assembled directly in
  * device memory the caller must set both truthfully: the tiled kernel trusts them.           */
@@ -228,6 +231,42 @@ int bc_summary(bc_ctx* ctx, const int32_t* d_cov, const double* d_ent, int64_t r
 int bc_amplicons(bc_ctx* ctx, const int32_t* d_cov, const double* d_ent, const double* d_sec,
                  int64_t ref_len, const int64_t* d_lo, const int64_t* d_hi, int32_t n_tiles,
                  double* d_out);
+
+/* ---- Multi-GPU: one process per GPU, RCCL over xGMI ---------------------------
+ * Counting needs no exchange: references are independent, so each rank owns whole references
+ * and runs the single-GPU path on them.  What crosses GPUs is small: the per-reference results
+ * the reference prints (main.py:469-595) gathered to rank 0, the reference order rank 0 chose
+ * (main.py:92 iterates a set, whose order is per process), and every reference's first
+ * out-of-range read (so all ranks raise the reference's first error).  The reference itself has
+ * no collective: this replaces nothing in it, it is what lets its per-reference loop
+ * (main.py:130-205) run on N GPUs.
+ * Rendezvous: rank 0 calls bc_comm_unique_id and hands the BC_COMM_ID_BYTES bytes to the other
+ * ranks out of band (basecount_amd/dist.py: a TCP socket next to MASTER_ADDR:MASTER_PORT); then
+ * every rank calls bc_comm_init with its own context (one GPU per rank).  Every call below but
+ * bc_gather_layout is collective: all ranks make it, in the same order.  Collectives run on the
+ * context's stream; the bc_*_bytes / _i64 / barrier calls are blocking, bc_gather_dev is
+ * stream-ordered and asynchronous.                                                            */
+#define BC_COMM_ID_BYTES 128
+typedef struct bc_comm bc_comm;
+int bc_comm_unique_id(uint8_t* id /* [BC_COMM_ID_BYTES] */);
+int bc_comm_init(bc_ctx* ctx, const uint8_t* id, int rank, int world, bc_comm** out);
+int bc_comm_destroy(bc_comm* comm);
+int bc_comm_rank(const bc_comm* comm, int* rank, int* world);
+int bc_comm_barrier(bc_comm* comm);
+/* h_recv[r * n + i] = rank r's h_send[i] (n is the same on every rank). */
+int bc_allgather_i64(bc_comm* comm, const int64_t* h_send, int64_t n, int64_t* h_recv);
+/* root's n bytes to every rank (n the same on every rank). */
+int bc_broadcast_bytes(bc_comm* comm, void* h_buf, int64_t n, int root);
+/* Ragged gather layout (host arithmetic, no GPU): offsets[r] = sum of sizes[0..r),
+ * offsets[world] = total.  BC_E_ARG on a negative size or an overflowing total.             */
+int bc_gather_layout(const int64_t* sizes, int world, int64_t* offsets /* [world + 1] */);
+/* Ragged gather to `root`: rank r sends n_r bytes; sizes[0..world) holds every n_r on every rank
+ * (exchange them first with bc_allgather_i64).  On root the payloads land concatenated in rank
+ * order at bc_gather_layout's offsets; other ranks' receive pointers are ignored.
+ *   bc_gather_bytes: host buffers, blocking (h_recv: offsets[world] bytes on root).
+ *   bc_gather_dev:   device buffers, stream-ordered on the context's stream, capturable.       */
+int bc_gather_bytes(bc_comm* comm, const void* h_send, int64_t n, void* h_recv, const int64_t* sizes, int root);
+int bc_gather_dev(bc_comm* comm, const void* d_send, int64_t n, void* d_recv, const int64_t* sizes, int root);
 
 /* Drop-in for count.bcount with host buffers: uploads, counts all 6 columns, downloads.
  * h_out: refLen x 6 uint32, ROW-major like the reference's vector<vector<unsigned>>

@@ -59,6 +59,11 @@ typedef struct bcio_records {
                                qual[2*seq_off[r] + i]  (so one offset addresses both)         */
     uint64_t seq_bytes;     /* = seq_off[n]                                                   */
     const int64_t* ref_span;/* [n] reference span: sum of M/D/N/=/X lengths                     */
+    const uint8_t* seq_event;/* the same SEQ bytes in the kernels' BC_SEQ_EVENT layout
+                                (basecount_hip.h): byte m of a record = its bases 2m (low
+                                nibble) and 2m+1 (high), pre-classified; built during the
+                                decode so the upload needs no device conversion pass          */
+    uint64_t seq_event_bytes;/* seq_bytes rounded up to 16, plus 16 zero bytes (padding)       */
 } bcio_records;
 
 /* Open and fully decode a BAM file with `nthreads` inflate/decode threads (<=0: hardware). */
@@ -96,6 +101,11 @@ typedef struct bcio_selection {
 } bcio_selection;
 
 int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_sel, bcio_selection* out);
+
+/* BAM-packed SEQ bytes -> BC_SEQ_EVENT (basecount_hip.h), on the host with `nthreads` threads
+ * (<= 0: hardware).  out_bytes >= nbytes rounded up to 16 plus 16; the tail is zero-filled.
+ * The decoder already provides this layout for a file's records (bcio_records.seq_event).   */
+int bcio_seq_to_event(const uint8_t* bam, int64_t nbytes, uint8_t* out, int64_t out_bytes, int nthreads);
 
 /* ---- writer: BAM records -> BGZF file (used by the synthetic generator) ----------------- */
 typedef struct bcio_write_spec {

@@ -42,6 +42,10 @@ def lib() -> C.CDLL:
         L.oracle_stats.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_double, C.c_double,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_stats.restype = None
+        L.oracle_bcount_mt.argtypes = L.oracle_bcount.argtypes + [C.c_int]
+        L.oracle_bcount_mt.restype = C.c_int
+        L.oracle_stats_mt.argtypes = L.oracle_stats.argtypes + [C.c_int]
+        L.oracle_stats_mt.restype = None
         _lib = L
     return _lib
 
@@ -50,9 +54,10 @@ def _p(a):
     return a.ctypes.data if a is not None and a.size else None
 
 
-def bcount(ref_len: int, mbq: int, b: dict):
+def bcount(ref_len: int, mbq: int, b: dict, nthreads: int = 0):
     """Oracle counts [ref_len][6] uint32 for a batch dict (bc_reads layout), plus
-    (bad_read, bad_pos) — (-1, -1) when no counted event fell outside the reference."""
+    (bad_read, bad_pos) — (-1, -1) when no counted event fell outside the reference.
+    nthreads > 0: the all-cores driver (mt_oracle.c), same results."""
     out = np.zeros((max(ref_len, 0), 6), np.uint32)
     br, bp = C.c_int64(-1), C.c_int64(-1)
     arrs = [np.ascontiguousarray(b[k], dt) for k, dt in
@@ -60,8 +65,13 @@ def bcount(ref_len: int, mbq: int, b: dict):
              ("seq_nib", np.uint32), ("cigar", np.uint32), ("seq", np.uint8))]
     q = b.get("qual")
     q = None if q is None else np.ascontiguousarray(q, np.uint8)
-    lib().oracle_bcount(int(ref_len), int(mbq), int(arrs[0].size), *[_p(a) for a in arrs], _p(q),
-                        _p(out) if out.size else None, C.byref(br), C.byref(bp))
+    args = [int(ref_len), int(mbq), int(arrs[0].size), *[_p(a) for a in arrs], _p(q),
+            _p(out) if out.size else None, C.byref(br), C.byref(bp)]
+    if nthreads > 0:
+        if lib().oracle_bcount_mt(*args, int(nthreads)) < 0:
+            raise MemoryError("oracle_bcount_mt: per-thread histograms")
+    else:
+        lib().oracle_bcount(*args)
     return out, (br.value, bp.value)
 
 
@@ -70,7 +80,7 @@ def norm_factors(show_n: bool):
     return 1 / math.log2(k), 1 / math.log2(k - 1)
 
 
-def stats(counts6: np.ndarray, show_n: bool):
+def stats(counts6: np.ndarray, show_n: bool, nthreads: int = 0):
     """(cov[L] i32, pc[k][L], ent[L], sec[L]) exactly as main.py:14-79 computes them."""
     c = np.ascontiguousarray(counts6, np.uint32)
     L = c.shape[0]
@@ -80,7 +90,10 @@ def stats(counts6: np.ndarray, show_n: bool):
     pc = np.zeros((k, L))
     ent = np.zeros(L)
     sec = np.zeros(L)
-    if L:
+    if L and nthreads > 0:
+        lib().oracle_stats_mt(_p(c), L, int(show_n), nf, nf2, _p(cov), _p(pc), _p(ent), _p(sec),
+                              int(nthreads))
+    elif L:
         lib().oracle_stats(_p(c), L, int(show_n), nf, nf2, _p(cov), _p(pc), _p(ent), _p(sec))
     return cov, pc, ent, sec
 
@@ -126,7 +139,7 @@ def summary(cov: np.ndarray, ent: np.ndarray, num_reads: int, ref: str, dp: int)
     L = int(cov.size)
     avg_cov = np.mean(cov.astype(np.int64))
     avg_ent = np.mean(ent)
-    pc_cov = 100 * (len([c for c in cov.tolist() if c != 0]) / L)
+    pc_cov = 100 * (int(np.count_nonzero(cov)) / L)  # len([c for c in coverages if c != 0])
     return {
         "reference_name": ref,
         "reference_length": round(L, dp),
@@ -205,9 +218,10 @@ def batch_from_bam(f, t, mmq):
                 cigar=f.cigar, seq=f.seq, qual=f.qual), int(idx.size)
 
 
-def summary_text(ref, counts6, show_n, num_reads, dp, tiles=None):
+def summary_text(ref, counts6, show_n, num_reads, dp, tiles=None, nthreads: int = 0):
     """main.py:469-595 text for one reference from oracle counts."""
-    cov, pc, ent, sec = stats(counts6, show_n)
+    cov, pc, ent, sec = stats(counts6, show_n, nthreads=nthreads)
+    del pc
     s = summary(cov, ent, num_reads, ref, dp)
     out = "".join(f"{kk}\t{v}\n" for kk, v in s.items())
     if tiles is not None:

@@ -21,10 +21,12 @@
 #include <math.h>
 #include <stdint.h>
 
-void oracle_stats(const uint32_t* counts6 /* [L][6] as returned by bcount */, int64_t L, int show_n, double nf,
-                  double nf2, int32_t* cov_out, double* pc /* [k][L] */, double* ent, double* sec) {
+/* positions [p0, p1) of a reference of L positions (the multi-threaded driver, mt_oracle.c,
+ * splits the positions; every position is independent) */
+void oracle_stats_range(const uint32_t* counts6, int64_t p0, int64_t p1, int64_t L, int show_n, double nf,
+                        double nf2, int32_t* cov_out, double* pc, double* ent, double* sec) {
     const int k = show_n ? 6 : 5;
-    for (int64_t p = 0; p < L; ++p) {
+    for (int64_t p = p0; p < p1; ++p) {
         int64_t c[6];
         int64_t cov = 0;
         for (int j = 0; j < k; ++j) {
@@ -61,4 +63,9 @@ void oracle_stats(const uint32_t* counts6 /* [L][6] as returned by bcount */, in
         }
         sec[p] = nf2 * s2;
     }
+}
+
+void oracle_stats(const uint32_t* counts6 /* [L][6] as returned by bcount */, int64_t L, int show_n, double nf,
+                  double nf2, int32_t* cov_out, double* pc /* [k][L] */, double* ent, double* sec) {
+    oracle_stats_range(counts6, 0, L, L, show_n, nf, nf2, cov_out, pc, ent, sec);
 }

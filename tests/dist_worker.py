@@ -15,7 +15,6 @@ sys.path.insert(0, REPO)
 from basecount_amd import main as M  # noqa: E402
 
 REFS = {"chrA": 1000, "chrB": 37, "chrC": 0, "chrD": 4000, "chrE": 250}
-ORDER = ["chrD", "chrA", "chrE", "chrC", "chrB"]  # stands in for the set order
 
 
 def fake_get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality=0,
@@ -26,11 +25,17 @@ def fake_get_basecounts(bam, references=None, min_base_quality=0, min_mapping_qu
     k = 6 if show_n_bases else 5
     refs = dict(REFS, chrC=3) if (_mode == "summary" and not os.environ.get("FAKE_EMPTY_REF")) else REFS
     nreads = {r: 3 * L // 7 + 1 for r, L in refs.items()}
-    owner = mine = None
-    mine = ORDER
+    from basecount_amd.dist import agree_order
+
+    # the set order of this process (PYTHONHASHSEED), as main.py:92 iterates it; with a group,
+    # rank 0's order (agree_order), exactly as the real get_basecounts does
+    order = list(set(REFS))
+    owner = None
+    mine = order
     if _group is not None:
-        owner = shard(ORDER, {r: refs[r] + 100 * nreads[r] for r in ORDER}, _group.world)
-        mine = [r for r in ORDER if owner[r] == _group.rank]
+        order = agree_order(_group, order)
+        owner = shard(order, {r: refs[r] + 100 * nreads[r] for r in order}, _group.world)
+        mine = [r for r in order if owner[r] == _group.rank]
     out = {}
     for ref in mine:
         L = refs[ref]
@@ -57,7 +62,7 @@ def fake_get_basecounts(bam, references=None, min_base_quality=0, min_mapping_qu
                         s["amplicons"] = (amp, [i % 3 == 0 for i in range(len(t))])
             out[ref] = {"summary": s, "num_reads": nreads[ref], "length": L}
     if _group is not None:
-        return out, owner, ORDER
+        return out, owner, order
     return out
 
 

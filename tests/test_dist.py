@@ -22,15 +22,15 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run(world: int, args, tmp_path, name, expect_fail=False, extra_env=None):
+def _run(world: int, args, tmp_path, name, expect_fail=False, extra_env=None, rank_env=None):
     out = tmp_path / f"{name}.out"
-    env = dict(os.environ, **(extra_env or {}), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+    env = dict(os.environ, **dict({"PYTHONHASHSEED": "0"}, **(extra_env or {})), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                WORLD_SIZE=str(world), BASECOUNT_DIST_BACKEND="gloo", CUDA_VISIBLE_DEVICES="",
                HIP_VISIBLE_DEVICES="")
     with open(out, "ab") as fh:
         procs = []
         for r in range(world):
-            e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r), **((rank_env or {}).get(r, {})))
             if world == 1:
                 for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
                     e.pop(v)
@@ -61,6 +61,41 @@ def test_cli_world2_matches_single_process(tmp_path, args):
     multi = _run(2, args, tmp_path, "multi")
     assert len(single) > 500
     assert multi == single
+
+
+@pytest.mark.parametrize("args", [["x.bam"], ["x.bam", "--summarise"]])
+def test_cli_ranks_with_different_hash_seeds(tmp_path, args):
+    """torchrun does not pin PYTHONHASHSEED: each rank iterates set(references) in its own order
+    (main.py:92).  Rank 0's order is broadcast (dist.agree_order), so the output is the single
+    process's with rank 0's seed."""
+    seeds = {0: {"PYTHONHASHSEED": "1"}, 1: {"PYTHONHASHSEED": "2"}}
+    single = _run(1, args, tmp_path, "single", extra_env={"PYTHONHASHSEED": "1"})
+    other = _run(1, args, tmp_path, "other", extra_env={"PYTHONHASHSEED": "2"})
+    assert single != other  # the two seeds do order the references differently
+    multi = _run(2, args, tmp_path, "multi", rank_env=seeds)
+    assert multi == single
+
+
+def test_gather_layout_ragged():
+    """bc_gather_layout (C-ABI, host arithmetic): rank payloads concatenated in rank order."""
+    import numpy as np
+
+    from basecount_amd.device import BcError
+    from basecount_amd.dist import gather_layout
+
+    for sizes in ([0], [5], [3, 0, 1003, 7], [0, 0, 0], list(range(8))):
+        offs = gather_layout(sizes)
+        assert offs == [0] + np.cumsum(sizes).tolist()
+        # emulate the root's receive buffer: every payload lands whole at its offset
+        payloads = [bytes([r + 1]) * n for r, n in enumerate(sizes)]
+        buf = bytearray(offs[-1])
+        for r, p in enumerate(payloads):
+            buf[offs[r]: offs[r + 1]] = p
+        assert [bytes(buf[offs[r]: offs[r + 1]]) for r in range(len(sizes))] == payloads
+    with pytest.raises(BcError):
+        gather_layout([4, -1])
+    with pytest.raises(BcError):
+        gather_layout([2 ** 62, 2 ** 62])
 
 
 def test_cli_world2_summary_with_bed(tmp_path):

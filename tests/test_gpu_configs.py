@@ -1,0 +1,144 @@
+"""The BASELINE configurations at full size through the product path, against the oracle
+(no config may stay untested on the GPU).
+
+  C5  24 GRCh38-sized contigs (3.09 Gb) x 50,000 reads: every contig through bc_pileup +
+      bc_summary (the sparse k_pileup_solo shape), coverage sums == events piled on all 24,
+      counts exact and entropies bit-identical on chr21, chr22, chrY and chr1 (249 Mb); then the
+      CLI's --summarise over a written BAM == the oracle's main.py:469-499 text for all 24.
+  C4  1,000,000 mixed-CIGAR reads + the 98-amplicon BED through the CLI's --summarise-with-bed
+      (the deep k_rc -> k_stats -> k_sum -> k_amplicon chain) == main.py:469-595 from the oracle.
+  C3  the same reads through the CLI's default per-position rows == main.py:454-466 from the
+      oracle, byte for byte.
+"""
+import contextlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from basecount_amd import device as D
+from basecount_amd import synth
+from basecount_amd.bam import BamFile, seq_to_event
+from basecount_amd.main import norm_factors
+from basecount_amd.scheme import load_scheme
+
+pytestmark = pytest.mark.gpu
+T = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return D.Context(0)
+
+
+def _run_cli(argv):
+    from basecount_amd.main import run
+
+    buf = io.BytesIO()
+    txt = io.TextIOWrapper(buf, encoding="utf-8", write_through=True)
+    with contextlib.redirect_stdout(txt):
+        run(argv)
+        txt.flush()
+    return buf.getvalue().decode()
+
+
+@pytest.fixture(scope="module")
+def c5():
+    return synth.make_config("c5")
+
+
+def test_c5_every_contig(ctx, c5):
+    rs = c5
+    ev = seq_to_event(rs.seq)
+    k = 5
+    nf, nf2 = norm_factors(k)
+    full = {"chr21", "chr22", "chrY", "chr1"}
+    for t, (name, L) in enumerate(zip(rs.references, rs.lengths)):
+        b = synth.batch_arrays(rs, t, 0)
+        r = D.DeviceReads(ctx, dict(b, seq_event=ev))
+        bufs = [ctx.alloc(n) for n in (4 * k * L, 4 * L, 8 * L, 8 * L, D.summary_work_bytes(L), 32)]
+        counts, cov, ent, sec, work, out = bufs
+        ctx.pileup(r, L, 0, k, nf, nf2, counts.ptr, cov.ptr, None, ent.ptr, sec.ptr)
+        ctx.summary(cov.ptr, ent.ptr, L, work.ptr, out.ptr)
+        assert ctx.range_error() == -1, name
+        hcov = cov.download(np.int32, L)
+        hent = ent.download(np.float64, L)
+        s = out.download(np.float64, 4)
+        # checksum of checksums: all-M reads without N put every event into the coverage
+        assert int(hcov.sum(dtype=np.int64)) == synth.ref_events(rs, t), name
+        c64 = hcov.astype(np.int64)
+        assert s[0] == np.mean(c64) and s[1] == np.mean(hent), name
+        assert int(s[2]) == int(np.count_nonzero(hcov)), name
+        del c64
+        if name in full:
+            exp, (br, _) = O.bcount(L, 0, b)
+            assert br == -1
+            got = counts.download(np.int32, k * L).reshape(k, L)
+            assert np.array_equal(got, exp[:, :k].T), name
+            del got
+            ocov, opc, oent, osec = O.stats(exp, False, nthreads=T)
+            del opc, exp
+            assert np.array_equal(hcov, ocov), name
+            assert np.array_equal(hent, oent), name  # bit-identical (glibc log2 on the device)
+            assert np.array_equal(sec.download(np.float64, L), osec), name
+            del ocov, oent, osec
+        for x in bufs:
+            x.free()
+        r.free()
+        del hcov, hent
+
+
+def test_c5_cli_summarise(c5, tmp_path):
+    bam = str(tmp_path / "c5.bam")
+    synth.write_bam(c5, bam)
+    got = _run_cli([bam, "--summarise"])
+    _, blocks = O.split_blocks(got, True)
+    assert sorted(blocks) == sorted(c5.references)
+    with BamFile(bam) as f:
+        for t, name in enumerate(f.references):
+            b, n = O.batch_from_bam(f, t, 0)
+            exp, (br, _) = O.bcount(f.lengths[t], 0, b)
+            assert br == -1
+            assert blocks[name] == O.summary_text(name, exp, False, n, 3, nthreads=T), name
+            del exp
+
+
+@pytest.fixture(scope="module")
+def c3_bam(tmp_path_factory):
+    rs = synth.make_config("c3")
+    d = tmp_path_factory.mktemp("c3")
+    bam = str(d / "c3.bam")
+    synth.write_bam(rs, bam)
+    bed = str(d / "scheme.bed")
+    with open(bed, "w") as fh:
+        fh.write(synth.artic_bed())
+    return bam, bed
+
+
+@pytest.mark.parametrize("args,mbq,mmq", [([], 0, 0),
+                                          (["--min-base-quality", "20", "--min-mapping-quality", "30"], 20, 30)])
+def test_c4_cli_summarise_with_bed(c3_bam, args, mbq, mmq):
+    bam, bed = c3_bam
+    got = _run_cli([bam, "--summarise-with-bed", bed] + args)
+    tiles = [(w["inside_start"], w["inside_end"]) for _, _, w in load_scheme(bed)]
+    assert len(tiles) == 98
+    with BamFile(bam) as f:
+        b, n = O.batch_from_bam(f, 0, mmq)
+        exp, (br, _) = O.bcount(f.lengths[0], mbq, b)
+        assert br == -1
+        assert got == O.summary_text(f.references[0], exp, False, n, 3, tiles=tiles)
+
+
+def test_c3_cli_rows(c3_bam):
+    bam, _ = c3_bam
+    got = _run_cli([bam])
+    with BamFile(bam) as f:
+        b, _ = O.batch_from_bam(f, 0, 0)
+        exp, (br, _) = O.bcount(f.lengths[0], 0, b)
+        assert br == -1
+        header = "\t".join(["reference", "position", "coverage", "num_a", "num_c", "num_g", "num_t",
+                            "num_ds", "pc_a", "pc_c", "pc_g", "pc_t", "pc_ds", "entropy",
+                            "secondary_entropy"]) + "\n"
+        assert got == header + O.rows_text(f.references[0], exp, False, False, 3)

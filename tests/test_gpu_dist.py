@@ -47,3 +47,60 @@ def test_cli_two_ranks_match_golden(tmp_path, case):
         gold = fh.read()
     assert single == gold
     assert multi == gold
+
+
+@pytest.mark.gpu
+def test_rccl_group_world1(monkeypatch):
+    """The product's RCCL group through the C-ABI (bc_comm_*) at world size 1 — the one size a
+    one-GPU box can run (RCCL refuses two ranks on one GPU; N > 1 runs in the driver's 8-GPU
+    bench): rendezvous, all-gather, broadcast, ragged host gather, device gather, barrier."""
+    import ctypes as C
+
+    import numpy as np
+
+    from basecount_amd import device as D
+    from basecount_amd.dist import Group, agree_order
+    from basecount_amd.main import context
+
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    g = Group("rccl")
+    try:
+        assert (g.world, g.rank) == (1, 0)
+        assert g.all_gather_ints([3, -7, 2 ** 40]) == [[3, -7, 2 ** 40]]
+        assert g.broadcast_bytes(b"chr1\x00chr2") == b"chr1\x00chr2"
+        assert g.broadcast_bytes(b"") == b""
+        assert agree_order(g, ["b", "a", "c"]) == ["b", "a", "c"]
+        assert g.gather_bytes(b"x" * 1003) == [b"x" * 1003]
+        assert g.gather_bytes(b"") == [b""]
+        g.barrier()
+        ctx = context()
+        src = ctx.alloc(64).upload(np.arange(16, dtype=np.float32))
+        dst = ctx.alloc(64)
+        sizes = np.array([64], np.int64)
+        D.check(D.lib().bc_gather_dev(g.h, src.ptr, 64, dst.ptr, sizes.ctypes.data, 0))
+        assert np.array_equal(dst.download(np.float32, 16), np.arange(16, dtype=np.float32))
+        # a wrong own size is an argument error, not a hang
+        bad = np.array([8], np.int64)
+        assert D.lib().bc_gather_dev(g.h, src.ptr, 64, dst.ptr, bad.ctypes.data, 0) == D.BC_E_ARG
+    finally:
+        g.close()
+
+
+@pytest.mark.gpu
+def test_cli_rccl_world1_matches_golden(tmp_path):
+    """get_basecounts with the RCCL group (world 1) through the whole sharded CLI path."""
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))["edge_summary_dp7"]
+    env = dict(os.environ, PYTHONPATH=REPO, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
+               PYTHONHASHSEED=str(man["hashseed"]))
+    code = ("import sys\n"
+            "from basecount_amd import main as M, dist\n"
+            "args = M.build_parser().parse_args(sys.argv[1:])\n"
+            "g = dist.Group('rccl')\n"
+            "M._run(args, None, 0, 0, 1000000, None, 7, g)\n"
+            "g.close()\n")
+    p = subprocess.run([sys.executable, "-c", code, man["bam"], *man["args"]], cwd=GOLD, env=env,
+                       capture_output=True, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    with gzip.open(os.path.join(GOLD, man["stdout"])) as fh:
+        assert p.stdout == fh.read()

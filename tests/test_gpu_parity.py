@@ -262,6 +262,7 @@ def test_fused_pileup_matches_oracle(ctx, seed, L, n, mbq, show_n, path):
     assert np.array_equal(cnt, exp[:, :k].T.astype(np.int32))
     assert np.array_equal(cov, ocov) and np.array_equal(pc, opc)
     assert np.max(np.abs(ent - oent)) <= 1e-6 and np.max(np.abs(sec - osec)) <= 1e-6
+    assert np.array_equal(ent, oent) and np.array_equal(sec, osec)  # glibc log2 on the device
 
 
 @pytest.mark.parametrize("path", ["tile", "rc"])
@@ -303,6 +304,8 @@ def test_kernel2_matches_oracle(ctx, show_n):
     assert np.max(np.abs(gent - ent)) <= tol and np.max(np.abs(gsec - sec)) <= tol
     exact = float(np.mean(gent == ent)), float(np.mean(gsec == sec))
     print(f"entropy bit-exact fraction: {exact[0]:.6f}, secondary: {exact[1]:.6f}")
+    # kernel 2 evaluates glibc's log2 algorithm (bc_log2.h): bit-identical to math.log2
+    assert exact == (1.0, 1.0)
     # printed values (3 dp) must agree
     for a, e in ((gent, ent), (gsec, sec)):
         assert [str(round(x, 3)) for x in a[:20000].tolist()] == [

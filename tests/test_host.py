@@ -226,3 +226,29 @@ def test_select_multi_chunk(tmp_path):
             assert sel.n_accepted == int(acc.sum())
             bad = np.nonzero(acc & (rs.tid == 1))[0]
             assert sel.keyerror_rec == bad[0] and sel.keyerror_ordinal == ordinal[bad[0]]
+
+
+def _event_numpy(seq: np.ndarray) -> np.ndarray:
+    """BC_SEQ_EVENT restated in numpy (basecount_hip.h): byte m = class(base 2m) | class(2m+1)
+    << 4 with A 1, C 2, G 4, T 8, N 3 and every other code 0."""
+    cls = np.zeros(16, np.uint8)
+    cls[[1, 2, 4, 8, 15]] = [1, 2, 4, 8, 3]
+    return cls[seq >> 4] | (cls[seq & 15] << 4)
+
+
+def test_decoder_emits_event_layout(mixed_bam):
+    """The decoder fills the kernels' sequence layout while decoding (no device
+    conversion pass per batch): identical to the standalone converter and to the restatement,
+    zero-padded to bc_seq_event_bytes."""
+    from basecount_amd.bam import seq_event_bytes, seq_to_event
+
+    rs, path = mixed_bam
+    with BamFile(path) as f:
+        n = f.seq.size
+        assert f.seq_event.size == seq_event_bytes(n) == (n + 15) // 16 * 16 + 16
+        assert np.array_equal(f.seq_event[:n], _event_numpy(f.seq))
+        assert not f.seq_event[n:].any()
+        assert np.array_equal(seq_to_event(f.seq, nthreads=3), f.seq_event)
+    every = np.arange(256, dtype=np.uint8)
+    assert np.array_equal(seq_to_event(every)[:256], _event_numpy(every))
+    assert seq_to_event(np.zeros(0, np.uint8)).tolist() == [0] * 16

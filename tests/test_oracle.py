@@ -115,3 +115,23 @@ def test_oracle_reproduces_reference_cli(golden, manifest, kind):
         assert got == exp_blocks, name
         n += 1
     assert n >= 10
+
+
+@pytest.mark.parametrize("nthreads", [1, 3, 8])
+def test_all_cores_oracle_matches_single_thread(nthreads):
+    """The all-cores CPU baseline (mt_oracle.c) computes exactly what the single-thread
+    restatement does, including the first out-of-range read."""
+    from basecount_amd import synth
+
+    rs = synth.make_reads([("a", 4_000)], 3_000, True, 12)
+    b = synth.batch_arrays(rs, 0, 0)
+    for L, mbq in ((4_000, 0), (4_000, 20), (2_500, 0)):
+        e1, bad1 = O.bcount(L, mbq, b)
+        e2, bad2 = O.bcount(L, mbq, b, nthreads=nthreads)
+        assert bad1 == bad2
+        if bad1[0] < 0:
+            assert np.array_equal(e1, e2)
+            for show_n in (False, True):
+                s1 = O.stats(e1, show_n)
+                s2 = O.stats(e1, show_n, nthreads=nthreads)
+                assert all(np.array_equal(x, y) for x, y in zip(s1, s2))

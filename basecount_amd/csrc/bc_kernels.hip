@@ -468,62 +468,119 @@ __device__ __forceinline__ long long block_sum_i64(long long v, long long* s_red
     return r;
 }
 
-// one workgroup (256 threads) per 8192 buffer: entropy pairwise sum, exact coverage sum, nnz
+// one workgroup (256 threads) per 8192 buffer: entropy pairwise sum, exact coverage sum, nnz.
+// A full buffer issues all its loads up front (8 x 16 B of coverage and 16 x 16 B of entropy per
+// thread) before any reduction, so a workgroup has its whole 96 KiB in flight at once; the
+// coverage sum and the non-zero count share one block reduction.
 __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const double* ent, int64_t L,
                                                     double* part_ent, long long* part_cov, long long* part_nz) {
     __shared__ double s_wave[4];
-    __shared__ long long s_red[4];
+    __shared__ long long s_red[8];
     __shared__ int s_off[128], s_len[128];
     __shared__ double s_val[128];
     const int64_t c0 = (int64_t)blockIdx.x * kNpBuf;
     const int m = (int)((L - c0) < kNpBuf ? (L - c0) : kNpBuf);
+    const int t = threadIdx.x;
     long long cs = 0, nz = 0;
-    for (int t = threadIdx.x; t < m; t += blockDim.x) {
-        const long long v = cov[c0 + t];
-        cs += v;
-        nz += v != 0;
-    }
-    cs = block_sum_i64(cs, s_red);
-    nz = block_sum_i64(nz, s_red);
     double e;
-    if (m == kNpBuf)
+    if (m == kNpBuf && ((uintptr_t)(cov + c0) & 15u) == 0) {
+        int4 cv[8];
+        const int4* c4 = (const int4*)(cov + c0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cv[j] = c4[t + 256 * j];
         e = pw_full8192([&](int i) { return ent[c0 + i]; }, s_wave);
-    else
-        e = pw_block(ent + c0, m, s_off, s_len, s_val);
-    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            cs += (long long)cv[j].x + cv[j].y + cv[j].z + cv[j].w;
+            nz += (cv[j].x != 0) + (cv[j].y != 0) + (cv[j].z != 0) + (cv[j].w != 0);
+        }
+    } else {
+        for (int i = t; i < m; i += blockDim.x) {
+            const long long v = cov[c0 + i];
+            cs += v;
+            nz += v != 0;
+        }
+        e = (m == kNpBuf) ? pw_full8192([&](int i) { return ent[c0 + i]; }, s_wave)
+                          : pw_block(ent + c0, m, s_off, s_len, s_val);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        cs += __shfl_down(cs, o);
+        nz += __shfl_down(nz, o);
+    }
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = cs;
+        s_red[4 + (t >> 6)] = nz;
+    }
+    __syncthreads();
+    if (t == 0) {
         part_ent[blockIdx.x] = e;
-        part_cov[blockIdx.x] = cs;
-        part_nz[blockIdx.x] = nz;
+        part_cov[blockIdx.x] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        part_nz[blockIdx.x] = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
     }
 }
 
 // One workgroup: the float64 fold over the per-buffer partials stays sequential (numpy adds the
-// buffers' pairwise sums in order), but 256 partials at a time are staged through LDS by the
-// whole block so thread 0 folds from LDS instead of waiting on one global load per buffer; the
-// integer sums are order-free and reduce in parallel.
+// buffers' pairwise sums in order: one dependent add per buffer is the floor).  The partials are
+// double-buffered through LDS, 1024 per round: the block loads round r+1 into registers while
+// thread 0 folds round r from LDS, so the fold never waits on a global load.  The integer sums
+// are order-free and reduce in parallel.
 __global__ __launch_bounds__(256) void k_sum_final(const double* part_ent, const long long* part_cov,
                                                    const long long* part_nz, int64_t nchunks, int64_t L,
                                                    double* out) {
-    __shared__ double s_buf[256];
-    __shared__ long long s_red[4];
+    constexpr int kR = 1024;
+    __shared__ double s_buf[2][kR];
+    __shared__ long long s_red[8];
+    const int t = threadIdx.x;
     double s = 0.0;
     long long cs = 0, nz = 0;
-    for (int64_t c0 = 0; c0 < nchunks; c0 += 256) {
-        const int64_t c = c0 + threadIdx.x;
-        const int m = (int)((nchunks - c0) < 256 ? (nchunks - c0) : 256);
-        if (c < nchunks) {
-            s_buf[threadIdx.x] = part_ent[c];
-            cs += part_cov[c];
-            nz += part_nz[c];
+    double v[4];
+    long long vc[4], vn[4];
+    auto load = [&](int64_t r0) {  // issue only: the values are consumed after the fold
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t c = r0 + t + 256 * j;
+            const bool in = c < nchunks;
+            v[j] = in ? part_ent[c] : 0.0;
+            vc[j] = in ? part_cov[c] : 0;
+            vn[j] = in ? part_nz[c] : 0;
         }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            s_buf[buf][t + 256 * j] = v[j];
+            cs += vc[j];
+            nz += vn[j];
+        }
+    };
+    load(0);
+    stash(0);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t r0 = 0; r0 < nchunks; r0 += kR) {
+        const bool more = r0 + kR < nchunks;
+        if (more) load(r0 + kR);  // in flight while thread 0 folds this round
+        if (t == 0) {
+            const int m = (int)((nchunks - r0) < kR ? (nchunks - r0) : kR);
+            const double* b = s_buf[cur];
+            for (int i = 0; i < m; ++i) s += b[i];
+        }
+        if (more) stash(cur ^ 1);
         __syncthreads();
-        if (threadIdx.x == 0)
-            for (int i = 0; i < m; ++i) s += s_buf[i];
-        __syncthreads();
+        cur ^= 1;
     }
-    cs = block_sum_i64(cs, s_red);
-    nz = block_sum_i64(nz, s_red);
-    if (threadIdx.x == 0) {
+    for (int o = 32; o > 0; o >>= 1) {
+        cs += __shfl_down(cs, o);
+        nz += __shfl_down(nz, o);
+    }
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = cs;
+        s_red[4 + (t >> 6)] = nz;
+    }
+    __syncthreads();
+    if (t == 0) {
+        cs = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        nz = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
         const double n = (double)L;
         out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
         out[1] = s / n;

@@ -185,7 +185,39 @@ def exc_line(stderr: str) -> str:
     return lines[last] if lines else ""
 
 
+# Cases added after the first generation (run with --add: the BAMs and the other cases are kept).
+# dp 17: more digits than a double holds, so the raw entropies are compared bit for bit through
+# the CLI (byte identity must not rest on rounding hiding one-ulp log2 differences).
+ADDED = {
+    "edge_dp17_shown": ("edge.bam", ["--decimal-places", "17", "--show-n-bases"]),
+    "edge_long_dp17": ("edge.bam", ["--long-format", "--decimal-places", "17"]),
+    "mixed_dp17": ("mixed.bam", ["--decimal-places", "17"]),
+    "mixed_bed_dp16": ("mixed.bam", ["--summarise-with-bed", "scheme.bed", "--decimal-places", "16"]),
+}
+
+
+def add_cases():
+    with open(os.path.join(HERE, "manifest.json")) as fh:
+        cases = json.load(fh)
+    os.chdir(HERE)
+    for name, (bam, args) in ADDED.items():
+        rc, out, err = run_ref([bam] + args)
+        rec = {"bam": bam, "args": args, "returncode": rc, "hashseed": "0"}
+        assert rc == 0, err
+        fn = f"cli/{name}.out.gz"
+        with open(os.path.join(HERE, fn), "wb") as fh:
+            fh.write(gzip.compress(out, compresslevel=9, mtime=0))
+        rec["stdout"] = fn
+        rec["sha256"] = hashlib.sha256(out).hexdigest()
+        cases[name] = rec
+        print(name, rc)
+    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+        json.dump(cases, fh, indent=1, sort_keys=True)
+
+
 def main():
+    if "--add" in sys.argv:
+        return add_cases()
     os.makedirs(os.path.join(HERE, "cli"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bcount"), exist_ok=True)
     synth.write_bam(synth.make_config("c1"), os.path.join(HERE, "c1.bam"), level=6)

@@ -448,6 +448,64 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
     return BC_OK;
 }
 
+int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, double nf, double nf2,
+                       int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent, double* d_sec, void* d_work) {
+    if (!c || !r || !d_work) return fail(BC_E_ARG, "NULL argument");
+    if (L <= 0) return fail(BC_E_ARG, "ref_len must be > 0 (np.mean of an empty list)");
+    const bool sparse_path = !bc::use_rc(*r, L, c->shape) && r->n_reads > 0;
+    if (!sparse_path) {
+        int rc = bc_pileup(c, r, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec);
+        if (rc) return rc;
+        if (!d_cov || !d_ent) return fail(BC_E_ARG, "NULL coverage / entropy");
+        DeviceGuard g(c->device);
+        Timed tm(c, BC_K_SUMMARY);
+        HIP_TRY(bc::launch_summary_partials(c->stream, d_cov, d_ent, L, d_work, 0));
+        return BC_OK;
+    }
+    // the argument checks of bc_pileup
+    if (k != 5 && k != 6) return fail(BC_E_ARG, "k must be 5 or 6");
+    if (!r->sorted) return fail(BC_E_ARG, "bc_pileup needs a coordinate-sorted batch (sorted == 1)");
+    if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+    if (r->seq_layout != BC_SEQ_EVENT) return fail(BC_E_ARG, "bc_pileup needs seq_layout == BC_SEQ_EVENT");
+    if ((uintptr_t)r->seq & 15u) return fail(BC_E_ARG, "bc_pileup needs a 16-byte aligned sequence buffer");
+    if (!d_counts || !d_cov || !d_ent || !d_sec) return fail(BC_E_ARG, "NULL output");
+    DeviceGuard g(c->device);
+    bc::SumParts parts = bc::summary_parts(d_work, L);
+    {
+        Timed tm(c, BC_K_PILEUP);
+        HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, d_counts, d_cov,
+                                        d_pc, d_ent, d_sec, c->d_err, c->shape, c->tile_waves, &parts));
+    }
+    const int64_t first = parts.fused ? parts.full_chunks : 0;
+    if (first < (L + 8191) / 8192) {  // the last, partial buffer (or all of them)
+        Timed tm(c, BC_K_SUMMARY);
+        HIP_TRY(bc::launch_summary_partials(c->stream, d_cov, d_ent, L, d_work, first));
+    }
+    return BC_OK;
+}
+
+int bc_summary_fold(bc_ctx* c, int n, const int64_t* ref_lens, void* const* d_works, double* const* d_outs) {
+    if (!c || n < 0 || (n > 0 && (!ref_lens || !d_works || !d_outs))) return fail(BC_E_ARG, "NULL argument");
+    for (int i = 0; i < n; ++i) {
+        if (ref_lens[i] <= 0) return fail(BC_E_ARG, "ref_len must be > 0 (np.mean of an empty list)");
+        if (!d_works[i] || !d_outs[i]) return fail(BC_E_ARG, "NULL work / output");
+    }
+    if (n == 0) return BC_OK;
+    DeviceGuard g(c->device);
+    Timed tm(c, BC_K_SUMMARY);
+    HIP_TRY(bc::launch_summary_fold(c->stream, n, ref_lens, d_works, d_outs));
+    return BC_OK;
+}
+
+int bc_pileup_summary(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, double nf, double nf2,
+                      int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent, double* d_sec, void* d_work,
+                      double* d_out) {
+    if (!d_out) return fail(BC_E_ARG, "NULL argument");
+    int rc = bc_pileup_partials(c, r, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec, d_work);
+    if (rc) return rc;
+    return bc_summary_fold(c, 1, &L, &d_work, &d_out);
+}
+
 int bc_graph_begin(bc_ctx* c) {
     if (!c) return fail(BC_E_ARG, "ctx is NULL");
     if (!c->stream) return fail(BC_E_ARG, "cannot capture the legacy default stream");

@@ -60,11 +60,20 @@ hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span);
 // to scratch_counts_out and it is zeroed again (k_stats)
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2,
                         int32_t* cov, double* pc, double* ent, double* sec, int32_t* scratch_counts_out = nullptr);
+// Summary partials (the per-8192-buffer sums bc_summary starts from): when the sparse sweep
+// runs with `parts`, it writes those of the whole buffers [0, full_chunks) itself (fused = true).
+struct SumParts {
+    double* ent;
+    long long* cov;
+    long long* nz;
+    bool fused;
+    int64_t full_chunks;
+};
 // shape: BC_SHAPE_*; tile_waves: 0 = from the depth, else 1/2/4/8 waves per tile
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
                                double* pc, double* ent, double* sec, unsigned long long* d_err, int shape = 0,
-                               int tile_waves = 0);
+                               int tile_waves = 0, SumParts* parts = nullptr);
 hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, int ncols, int32_t* counts,
                      unsigned long long* d_err);
 // bc_pileup / bc_count choose the read-chunked k_rc over the tiled k_pileup when a tile would
@@ -74,7 +83,12 @@ bool use_rc(const bc_reads& r, int64_t L, int shape);
 constexpr int kTileMaxSpan = 4096;  // beyond this span the tiled kernel's look-back gets too long
 size_t summary_work_bytes(int64_t L);
 hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
-                          double* out);
+                          double* out, int64_t first_chunk = 0);
+hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
+                                   int64_t first_chunk);
+hipError_t launch_summary_fold(hipStream_t s, int n, const int64_t* L, void* const* work, double* const* out);
+// the partial arrays inside a summary work buffer
+SumParts summary_parts(void* work, int64_t L);
 hipError_t launch_amplicons(hipStream_t s, const int32_t* cov, const double* ent, const double* sec,
                             int64_t L, const int64_t* lo, const int64_t* hi, int n_tiles, double* out);
 

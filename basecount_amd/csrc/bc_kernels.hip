@@ -8,6 +8,8 @@
 //
 // Integer scatter, not a contraction: no MFMA.  Kernel 1 is bound by HBM (read records) and by
 // the LDS atomic rate; see DESIGN.md for the roofline accounting.
+#include <cstring>
+
 #include "bc_internal.h"
 #include "bc_log2.h"
 
@@ -473,12 +475,14 @@ __device__ __forceinline__ long long block_sum_i64(long long v, long long* s_red
 // thread) before any reduction, so a workgroup has its whole 96 KiB in flight at once; the
 // coverage sum and the non-zero count share one block reduction.
 __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const double* ent, int64_t L,
-                                                    double* part_ent, long long* part_cov, long long* part_nz) {
+                                                    double* part_ent, long long* part_cov, long long* part_nz,
+                                                    int64_t first_chunk) {
     __shared__ double s_wave[4];
     __shared__ long long s_red[8];
     __shared__ int s_off[128], s_len[128];
     __shared__ double s_val[128];
-    const int64_t c0 = (int64_t)blockIdx.x * kNpBuf;
+    const int64_t chunk = first_chunk + blockIdx.x;
+    const int64_t c0 = chunk * kNpBuf;
     const int m = (int)((L - c0) < kNpBuf ? (L - c0) : kNpBuf);
     const int t = threadIdx.x;
     long long cs = 0, nz = 0;
@@ -513,23 +517,41 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const do
     }
     __syncthreads();
     if (t == 0) {
-        part_ent[blockIdx.x] = e;
-        part_cov[blockIdx.x] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-        part_nz[blockIdx.x] = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
+        part_ent[chunk] = e;
+        part_cov[chunk] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        part_nz[chunk] = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
     }
 }
 
-// One workgroup: the float64 fold over the per-buffer partials stays sequential (numpy adds the
-// buffers' pairwise sums in order: one dependent add per buffer is the floor).  The partials are
-// double-buffered through LDS, 1024 per round: the block loads round r+1 into registers while
-// thread 0 folds round r from LDS, so the fold never waits on a global load.  The integer sums
-// are order-free and reduce in parallel.
-__global__ __launch_bounds__(256) void k_sum_final(const double* part_ent, const long long* part_cov,
-                                                   const long long* part_nz, int64_t nchunks, int64_t L,
-                                                   double* out) {
+// The float64 fold over the per-buffer partials stays sequential (numpy adds the buffers'
+// pairwise sums in order: one dependent add per buffer is the floor).  One workgroup per
+// reference, so the folds of several references (bc_summary_fold) run side by side.  The
+// partials are double-buffered through LDS, 1024 per round: the block loads round r+1 into
+// registers while thread 0 folds round r from LDS in groups of 8 (loads of a group issued
+// together), so the fold never waits on a global load.  The integer sums are order-free and
+// reduce in parallel.
+struct FoldRef {
+    const double* pe;
+    const long long* pc;
+    const long long* pn;
+    int64_t nchunks;
+    int64_t L;
+    double* out;
+};
+constexpr int kFoldMax = 24;  // references per launch (kernel arguments by value)
+struct FoldArgs {
+    FoldRef ref[kFoldMax];
+};
+
+__global__ __launch_bounds__(256) void k_sum_final(FoldArgs FA) {
     constexpr int kR = 1024;
     __shared__ double s_buf[2][kR];
     __shared__ long long s_red[8];
+    const FoldRef& R = FA.ref[blockIdx.x];
+    const double* part_ent = R.pe;
+    const long long* part_cov = R.pc;
+    const long long* part_nz = R.pn;
+    const int64_t nchunks = R.nchunks;
     const int t = threadIdx.x;
     double s = 0.0;
     long long cs = 0, nz = 0;
@@ -563,7 +585,15 @@ __global__ __launch_bounds__(256) void k_sum_final(const double* part_ent, const
         if (t == 0) {
             const int m = (int)((nchunks - r0) < kR ? (nchunks - r0) : kR);
             const double* b = s_buf[cur];
-            for (int i = 0; i < m; ++i) s += b[i];
+            int i = 0;
+            for (; i + 8 <= m; i += 8) {
+                double w[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) w[u] = b[i + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s += w[u];
+            }
+            for (; i < m; ++i) s += b[i];
         }
         if (more) stash(cur ^ 1);
         __syncthreads();
@@ -581,11 +611,11 @@ __global__ __launch_bounds__(256) void k_sum_final(const double* part_ent, const
     if (t == 0) {
         cs = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
         nz = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
-        const double n = (double)L;
-        out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
-        out[1] = s / n;
-        out[2] = (double)nz;
-        out[3] = (double)cs;
+        const double n = (double)R.L;
+        R.out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
+        R.out[1] = s / n;
+        R.out[2] = (double)nz;
+        R.out[3] = (double)cs;
     }
 }
 
@@ -754,14 +784,48 @@ size_t summary_work_bytes(int64_t L) {
     return (size_t)(nc > 0 ? nc : 1) * 24;
 }
 
-hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work, double* out) {
+SumParts summary_parts(void* work, int64_t L) {
     const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
-    double* pe = (double*)work;
-    long long* pcv = (long long*)(pe + (nc > 0 ? nc : 1));
-    long long* pnz = pcv + (nc > 0 ? nc : 1);
-    if (nc > 0) hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)nc), dim3(256), 0, s, cov, ent, L, pe, pcv, pnz);
-    hipLaunchKernelGGL(k_sum_final, dim3(1), dim3(256), 0, s, pe, pcv, pnz, nc, L, out);
+    SumParts P;
+    P.ent = (double*)work;
+    P.cov = (long long*)(P.ent + (nc > 0 ? nc : 1));
+    P.nz = P.cov + (nc > 0 ? nc : 1);
+    P.fused = false;
+    P.full_chunks = 0;
+    return P;
+}
+
+// first_chunk > 0: the partials of the buffers before it are already in the work buffer (written
+// by the sparse pileup sweep, bc_pileup_summary); only the rest are computed here
+hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
+                                   int64_t first_chunk) {
+    const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
+    const SumParts P = summary_parts(work, L);
+    if (nc > first_chunk)
+        hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)(nc - first_chunk)), dim3(256), 0, s, cov, ent, L, P.ent, P.cov,
+                           P.nz, first_chunk);
     return hipGetLastError();
+}
+
+hipError_t launch_summary_fold(hipStream_t s, int n, const int64_t* L, void* const* work, double* const* out) {
+    for (int i0 = 0; i0 < n; i0 += kFoldMax) {
+        FoldArgs FA;
+        std::memset(&FA, 0, sizeof FA);
+        const int m = n - i0 < kFoldMax ? n - i0 : kFoldMax;
+        for (int i = 0; i < m; ++i) {
+            const SumParts P = summary_parts(work[i0 + i], L[i0 + i]);
+            FA.ref[i] = FoldRef{P.ent, P.cov, P.nz, (L[i0 + i] + kNpBuf - 1) / kNpBuf, L[i0 + i], out[i0 + i]};
+        }
+        hipLaunchKernelGGL(k_sum_final, dim3((unsigned)m), dim3(256), 0, s, FA);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work, double* out,
+                          int64_t first_chunk) {
+    hipError_t e = launch_summary_partials(s, cov, ent, L, work, first_chunk);
+    if (e != hipSuccess) return e;
+    return launch_summary_fold(s, 1, &L, &work, &out);
 }
 
 hipError_t launch_amplicons(hipStream_t s, const int32_t* cov, const double* ent, const double* sec, int64_t L,

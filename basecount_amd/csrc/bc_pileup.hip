@@ -60,6 +60,12 @@ struct PileArgs {
     int64_t seq_words;   // readable 32-bit words of seq (bc_seq_event_bytes / 4)
     int64_t qual_bytes;
     int64_t tiles_per_wave;  // k_pileup_solo: consecutive tiles swept by one wave
+    // k_pileup_solo with summary partials (bc_pileup_summary): numpy's per-8192-buffer pairwise
+    // entropy sums and the exact coverage / non-zero sums of the buffers [0, full_chunks)
+    double* part_ent;
+    long long* part_cov;
+    long long* part_nz;
+    int64_t full_chunks;
     int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 4 no walk, 8 no stats
                  // math, 16 no stores, 32 no sequence staging
     unsigned long long* trace;  // diagnostic only (BC_TRACE): per-wave phase stamps, else null
@@ -655,7 +661,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
 // Kernel 2 for one position from its counts (main.py:29-53 in CPython's order, the same
 // arithmetic as tile_terms + the ordered sums of k_pileup), written by the position's lane.
 template <int K>
-__device__ __forceinline__ void pos_stats(const PileArgs& A, const uint32_t* c, int64_t P) {
+__device__ __forceinline__ double pos_stats(const PileArgs& A, const uint32_t* c, int64_t P) {
     const int64_t L = A.L;
     int64_t cov = 0;
     int am = 0;
@@ -692,6 +698,40 @@ __device__ __forceinline__ void pos_stats(const PileArgs& A, const uint32_t* c, 
     }
     A.ent[P] = h;
     A.sec[P] = h2;
+    return h;
+}
+
+// numpy's pairwise_sum of one 128-element leaf (pw_leaf of bc_kernels.hip for n = 128) from two
+// consecutive tiles' entropies, one per lane: r_j = a[j] + a[8 + j] + ... + a[120 + j] in that
+// order (eight accumulators), then ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)).  The first
+// tile's half of the chains (leaf_half) is taken when that tile is done, so only its 8
+// accumulators stay live; leaf_finish adds the second tile's values and combines.  Every lane
+// returns the leaf.
+__device__ __forceinline__ double leaf_half(double ea, int lane) {
+    const int j = lane & 7;
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = __shfl(ea, 8 * i + j);
+    double r = v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) r = r + v[i];
+    return r;
+}
+__device__ __forceinline__ double leaf_finish(double r, double eb, int lane) {
+    const int j = lane & 7;
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = __shfl(eb, 8 * i + j);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r = r + v[i];
+    const double r01 = r + __shfl(r, j + 1);      // lanes 0, 2, 4, 6: r_j + r_j+1
+    const double r03 = r01 + __shfl(r01, j + 2);  // lanes 0, 4
+    return __shfl(r03, 0) + __shfl(r03, 4);
+}
+
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
 // Move a read cursor forward to the first index >= cur whose pos >= key (pos is sorted and the
@@ -718,7 +758,7 @@ __device__ __forceinline__ void advance_cursor(const int32_t* pos, int64_t n, in
 // Sparse batches: every wave owns a contiguous run of tiles and sweeps it with two read cursors
 // (no per-tile search), walks the few reads of each tile alone, and computes the statistics of
 // its own positions in registers: no block barriers at all.  Empty tiles only store.
-template <bool QUAL, int K, bool STATS>
+template <bool QUAL, int K, bool STATS, bool SUMP>
 __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     const int lane = threadIdx.x & 63;
@@ -739,6 +779,13 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     int64_t wlo_base = lo, whi_base = hi;
     int32_t wlo = lo + lane < A.n ? A.pos[lo + lane] : INT32_MAX;
     int32_t whi = hi + lane < A.n ? A.pos[hi + lane] : INT32_MAX;
+    // SUMP: the wave's tiles start on a buffer boundary (tiles_per_wave is a multiple of 128), so
+    // it sees whole 8192-position buffers: leaves of two tiles, merged into the buffer's pairwise
+    // tree (numpy splits 8192 evenly down to 128): the leaves wait in LDS (64 per wave) and are
+    // added pairwise across the lanes once the buffer is complete
+    double e_prev = 0.0;
+    double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + 64 * wave;
+    long long sum_cov = 0, sum_nz = 0;
     for (int64_t t = t_begin; t < t_end; ++t) {
         const int64_t t0 = t * kTile;
         const int64_t P = t0 + lane;
@@ -788,7 +835,41 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
                 if (A.accumulate) cnt[c] += (uint32_t)*dst;
                 *dst = (int32_t)cnt[c];
             }
-            if (STATS) pos_stats<K>(A, cnt, P);
+            if (STATS) {
+                const double h = pos_stats<K>(A, cnt, P);
+                if (SUMP) {
+                    static_assert(kNpBuf == 8192 && kNpBuf == 128 * kTile, "buffers of 128 tiles");
+                    const int64_t ch = t0 >> 13;  // 8192-position buffer
+                    if (ch < A.full_chunks) {
+                        const uint32_t cov = cnt[0] + cnt[1] + cnt[2] + cnt[3] + cnt[4] + (K == 6 ? cnt[5] : 0u);
+                        sum_cov += cov;
+                        sum_nz += cov != 0;
+                        if (t & 1) {
+                            const double lf = leaf_finish(e_prev, h, lane);
+                            const int leaf = (int)((t >> 1) & 63);
+                            if (lane == 0) myleaves[leaf] = lf;
+                            if (leaf == 63) {  // the buffer is complete: its 64 leaves, pairwise
+                                __builtin_amdgcn_wave_barrier();
+                                double v = myleaves[lane];
+#pragma unroll
+                                for (int l = 1; l < 64; l <<= 1) {  // left (lower lanes) + right
+                                    const double w = __shfl_down(v, l);
+                                    if ((lane & (2 * l - 1)) == 0) v = v + w;
+                                }
+                                const long long cs = wave_sum_i64(sum_cov), nz = wave_sum_i64(sum_nz);
+                                if (lane == 0) {
+                                    A.part_ent[ch] = v;
+                                    A.part_cov[ch] = cs;
+                                    A.part_nz[ch] = nz;
+                                }
+                                sum_cov = sum_nz = 0;
+                            }
+                        } else {
+                            e_prev = leaf_half(h, lane);  // the first tile's half of the chains
+                        }
+                    }
+                }
+            }
         }
     }
 }
@@ -817,7 +898,7 @@ PileArgs make_args(const bc_reads& r, int64_t L, uint32_t mbq) {
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
                                double* pc, double* ent, double* sec, unsigned long long* d_err, int shape,
-                               int tile_waves) {
+                               int tile_waves, SumParts* parts) {
     PileArgs A = make_args(r, L, mbq);
     const int64_t reach = max_end > L ? max_end : L;  // edge tiles up to the furthest read end
     A.n_tiles = (reach + kTile - 1) / kTile;
@@ -841,18 +922,33 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
     while (S < 8 && per_tile > 48.0 * S) S *= 2;
     if (tile_waves == 1 || tile_waves == 2 || tile_waves == 4 || tile_waves == 8) S = tile_waves;
     A.S = S;
+    if (parts) parts->fused = false;
     if (S == 1 && shape != BC_SHAPE_TILE_NO_SOLO) {
         // sparse: waves sweep contiguous tile runs; ~2 rounds of resident waves (256 CUs x 16)
         const int nw = 4;
         const int64_t target_waves = 256 * 16 * 2;
         A.tiles_per_wave = (A.n_tiles + target_waves - 1) / target_waves;
         if (A.tiles_per_wave < 1) A.tiles_per_wave = 1;
+        const bool sump = parts && stats && L >= kNpBuf;
+        if (sump) {  // whole 8192-position buffers per wave: the summary partials come for free
+            A.tiles_per_wave = (A.tiles_per_wave + 127) / 128 * 128;
+            A.part_ent = parts->ent;
+            A.part_cov = parts->cov;
+            A.part_nz = parts->nz;
+            A.full_chunks = L / kNpBuf;
+            parts->fused = true;
+            parts->full_chunks = A.full_chunks;
+        }
         const int64_t waves = (A.n_tiles + A.tiles_per_wave - 1) / A.tiles_per_wave;
         int64_t blocks = (waves + nw - 1) / nw;
         blocks = (blocks + 7) / 8 * 8;  // a multiple of the XCD count (see the kernel's tile mapping)
         const dim3 grid((unsigned)blocks), block(64 * nw);
-        const size_t lds = (size_t)nw * (kRecBytes + kStageRegion);
-#define BC_SOLO(Q, KK, ST) hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST>), grid, block, lds, s, A)
+        const size_t lds = (size_t)nw * (kRecBytes + kStageRegion) + (sump ? (size_t)nw * 64 * 8 : 0);
+#define BC_SOLO(Q, KK, ST)                                                                   \
+    do {                                                                                     \
+        if (sump) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true>), grid, block, lds, s, A); \
+        else hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST, false>), grid, block, lds, s, A);  \
+    } while (0)
         if (mbq > 0) {
             if (k == 5) {
                 if (stats) BC_SOLO(true, 5, true); else BC_SOLO(true, 5, false);

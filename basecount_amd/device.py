@@ -84,6 +84,11 @@ def lib() -> C.CDLL:
                             C.POINTER(i64)], C.c_int),
         "bc_pileup": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, dbl, dbl, vp, vp, vp, vp, vp],
                       C.c_int),
+        "bc_pileup_summary": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, dbl, dbl, vp, vp, vp, vp, vp,
+                               vp, vp], C.c_int),
+        "bc_pileup_partials": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, dbl, dbl, vp, vp, vp, vp, vp,
+                                vp], C.c_int),
+        "bc_summary_fold": ([vp, C.c_int, vp, vp, vp], C.c_int),
         "bc_graph_begin": ([vp], C.c_int),
         "bc_graph_end": ([vp, C.POINTER(vp)], C.c_int),
         "bc_graph_launch": ([vp, vp], C.c_int),
@@ -263,6 +268,28 @@ class Context:
         r = reads.r if isinstance(reads, DeviceReads) else reads
         check(lib().bc_pileup(self.h, C.byref(r), int(L), int(mbq), int(k), float(nf), float(nf2),
                               d_counts, d_cov, d_pc, d_ent, d_sec))
+
+    def pileup_summary(self, reads, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec, d_work,
+                       d_out):
+        """bc_pileup + bc_summary in one call (the sparse sweep computes the summary partials)."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        check(lib().bc_pileup_summary(self.h, C.byref(r), int(L), int(mbq), int(k), float(nf),
+                                      float(nf2), d_counts, d_cov, d_pc, d_ent, d_sec, d_work, d_out))
+
+    def pileup_partials(self, reads, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec, d_work):
+        """bc_pileup_partials: pileup + the summary's per-buffer partials (fold them with
+        summary_fold)."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        check(lib().bc_pileup_partials(self.h, C.byref(r), int(L), int(mbq), int(k), float(nf),
+                                       float(nf2), d_counts, d_cov, d_pc, d_ent, d_sec, d_work))
+
+    def summary_fold(self, lens, works, outs) -> None:
+        """bc_summary_fold over several references (device pointers works / outs)."""
+        n = len(lens)
+        la = (C.c_int64 * max(1, n))(*[int(x) for x in lens])
+        wa = (C.c_void_p * max(1, n))(*works)
+        oa = (C.c_void_p * max(1, n))(*outs)
+        check(lib().bc_summary_fold(self.h, n, la, wa, oa))
 
     def capture(self, fn) -> "Graph":
         """Record the compute calls made by fn() into a hipGraph (replay with Graph.launch)."""

@@ -461,7 +461,15 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
     outs = _alloc_outputs(ctx, k, L, want_pc=(mode == "rows"))
     hist = ctx.alloc(4 * ncols * L)
     pc_ptr = outs["pc"].ptr if outs["pc"] else None
-    if reads.sorted:
+    work = dout = None
+    if mode != "rows":
+        work = ctx.alloc(D.summary_work_bytes(L))
+        dout = ctx.alloc(32)
+    if reads.sorted and mode != "rows":
+        # pileup + summary: the sparse sweep computes numpy's buffer partials in registers
+        ctx.pileup_summary(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr,
+                           outs["ent"].ptr, outs["sec"].ptr, work.ptr, dout.ptr)
+    elif reads.sorted:
         ctx.pileup(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
                    outs["sec"].ptr)
     else:
@@ -469,14 +477,13 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
         ctx.count(reads, L, mbq, ncols, hist.ptr)
         ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
                   outs["sec"].ptr)
+        if mode != "rows":
+            ctx.summary(outs["cov"].ptr, outs["ent"].ptr, L, work.ptr, dout.ptr)
     bad = ctx.range_error()
     if mode == "rows":
         counts = hist.download(np.int32, ncols * L).reshape(ncols, L)
         return _download(outs, counts, k, L), bad
     res = {"L": L}
-    work = ctx.alloc(D.summary_work_bytes(L))
-    dout = ctx.alloc(32)
-    ctx.summary(outs["cov"].ptr, outs["ent"].ptr, L, work.ptr, dout.ptr)
     s = dout.download(np.float64, 4)
     res.update(avg_cov=np.float64(s[0]), avg_ent=np.float64(s[1]), nnz=int(s[2]))
     if tiles is not None and len(tiles):

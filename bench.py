@@ -15,8 +15,11 @@ summaries are gathered to rank 0 over RCCL once after the timed region (``gather
 ``extra`` carries the other BASELINE shapes, each timed the same way with its own roofline:
   * c3 (N=1): 1,000,000 mixed-CIGAR reads on the same contig (deep: k_rc + k_stats);
   * c5 (every N): 24 GRCh38-sized contigs (3.09 Gb) x 50,000 reads, sharded over the ranks (LPT,
-    strong scaling), summary-shaped (main.py:469-499: no per-position percentages), each step
-    ending with the RCCL gather of every contig's summary to rank 0 (``gather_us``).
+    strong scaling), summary-shaped (main.py:469-499: no per-position percentages; every
+    per-position count, coverage and entropy is still written), bc_pileup_partials per contig
+    (the sparse sweep also computes numpy's buffer partial sums) and one bc_summary_fold for all
+    of the rank's contigs, each step ending with the RCCL gather of every contig's summary to
+    rank 0 (``gather_us``).
 At N=1 rank 0 also times the reference's CPU path (its own compiled count.cpp + get_stats, one
 core), the all-cores C restatement (``cpu_baseline_all_cores``), and the CLI end to end on the C2
 BAM (decode, upload, kernels, formatting: ``e2e``).
@@ -50,7 +53,8 @@ WORKLOADS = {
           "all-M CIGAR; contigs sharded over the ranks, summary + RCCL gather to rank 0 per step",
 }
 KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "rc": "k_rc (read-chunked kernel 1)",
-                "stats": "k_stats (kernel 2)", "summary": "k_sum_chunks + k_sum_final (summary)"}
+                "stats": "k_stats (kernel 2)",
+                "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)"}
 
 
 def read_bytes(b: dict, mbq: int, l_seq: np.ndarray) -> int:
@@ -237,10 +241,16 @@ class Workload:
     def step(self):
         ctx = self.ctx
         for i, (_, L, _, reads, o) in enumerate(self.work):
-            ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
-                       o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
-            if self.summarise:
-                ctx.summary(o["cov"].ptr, o["ent"].ptr, L, o["swork"].ptr, self.d_sum.ptr + 32 * i)
+            pc = o["pc"].ptr if o["pc"] is not None else None
+            if self.summarise:  # kernels 1 + 2 and the summary's per-buffer partial sums
+                ctx.pileup_partials(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr,
+                                    o["cov"].ptr, pc, o["ent"].ptr, o["sec"].ptr, o["swork"].ptr)
+            else:
+                ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
+                           pc, o["ent"].ptr, o["sec"].ptr)
+        if self.summarise:  # every contig's sequential fold, side by side (bc_summary_fold)
+            ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
+                             [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
 
     def count_only(self):
         for _, L, _, reads, o in self.work:
@@ -250,10 +260,6 @@ class Workload:
         for _, L, _, _, o in self.work:
             self.ctx.stats(o["counts"].ptr, L, self.k, self.nf, self.nf2, o["cov"].ptr,
                            o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
-
-    def summary_only(self):
-        for i, (_, L, _, _, o) in enumerate(self.work):
-            self.ctx.summary(o["cov"].ptr, o["ent"].ptr, L, o["swork"].ptr, self.d_sum.ptr + 32 * i)
 
     def parity(self) -> bool:
         """Counts exact and entropy within 1e-6 against the oracle on the rank's smallest contig;
@@ -391,7 +397,21 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
 
     reps = max(3, min(steps, 100))
     kern_s = {}
-    if "pileup" in launched:
+    if summarise:
+        # the step's own launches, each bracketed by hipEvents (library timing facility): the
+        # sweep (with its partial sums) and the summary's tail + fold, per step
+        reps_t = max(2, min(steps, 5))
+        ctx.sync()
+        ctx.timing(True)
+        for _ in range(reps_t):
+            wl.step()
+        rep = ctx.timing_report()
+        ctx.timing(False)
+        for name in ("pileup", "rc", "stats", "summary"):
+            if name in rep:
+                n_launch, mean_us = rep[name]
+                kern_s[name] = n_launch * mean_us * 1e-6 / reps_t
+    elif "pileup" in launched:
         def pile_only():
             for _, L, _, reads, o in wl.work:
                 ctx.pileup(reads, L, wl.mbq, wl.k, wl.nf, wl.nf2, o["counts"].ptr, o["cov"].ptr,
@@ -399,11 +419,9 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         # eager back-to-back launches: the kernel's own average duration (what rocprofv3's kernel
         # trace reports); a graph replay hides part of the launch gap and would flatter it
         kern_s["pileup"] = region(pile_only, reps)
-    if "rc" in launched:  # deep batches: k_rc + k_stats (bc_count on the same batch: k_rc alone)
+    if "rc" in launched and not summarise:  # deep: k_rc + k_stats (bc_count: k_rc alone)
         kern_s["rc"] = region(wl.count_only, reps)
         kern_s["stats"] = region(wl.stats_only, reps)
-    if summarise:
-        kern_s["summary"] = region(wl.summary_only, reps)
     gather_us = None
     if gather is not None:
         if group is not None:

@@ -224,6 +224,25 @@ size_t bc_summary_work_bytes(int64_t ref_len);
 int bc_summary(bc_ctx* ctx, const int32_t* d_cov, const double* d_ent, int64_t ref_len,
                void* d_work, double* d_out);
 
+/* Fused pileup + summary (main.py:469-499's numbers for one reference, as bc_pileup followed by
+ * bc_summary, bit-identical): for sparse batches the pileup sweep computes numpy's per-buffer
+ * partial sums while the statistics are still in registers, so the per-position coverage and
+ * entropies are not read back; other batches run bc_pileup + bc_summary.  Arguments as bc_pileup
+ * (all per-position outputs written) plus d_work (bc_summary_work_bytes(ref_len)) and d_out (4
+ * doubles, as bc_summary).  ref_len must be > 0.                                              */
+int bc_pileup_summary(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality, int k,
+                      double nf, double nf2, int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent,
+                      double* d_sec, void* d_work, double* d_out);
+/* The same in two parts, for several references: bc_pileup_partials leaves numpy's per-buffer
+ * partial sums of one reference in d_work; bc_summary_fold then folds n references' partials
+ * (one workgroup each, side by side: the fold is one dependent add per 8192 positions, the only
+ * sequential step of the summary) and writes each reference's 4 doubles to d_outs[i].
+ * ref_lens / d_works / d_outs are host arrays of n entries (device pointers).                  */
+int bc_pileup_partials(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality, int k,
+                       double nf, double nf2, int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent,
+                       double* d_sec, void* d_work);
+int bc_summary_fold(bc_ctx* ctx, int n, const int64_t* ref_lens, void* const* d_works, double* const* d_outs);
+
 /* Amplicon vectors (main.py:501-551): for each tile t with inclusive window
  * [lo[t], hi[t]] (already clipped to [0, ref_len-1]; lo > hi = empty), np.mean and np.median of
  * coverage, entropy and secondary entropy over the window.  d_out: [n_tiles][6] f64 device

@@ -465,3 +465,70 @@ def test_full_size_c3_fused_pileup(ctx, path):
     ocov, opc, oent, osec = O.stats(exp, False)
     assert np.array_equal(cov, ocov) and np.array_equal(pc, opc)
     assert np.max(np.abs(ent - oent)) <= 1e-6 and np.max(np.abs(sec - osec)) <= 1e-6
+
+
+@pytest.mark.parametrize("L,n,mbq,show_n", [
+    (8192 * 9, 3_000, 0, False),          # whole buffers only
+    (8192 * 9 + 517, 3_000, 20, True),    # a partial last buffer (computed by the tail kernel)
+    (8191, 400, 0, False),                # no whole buffer
+    (200_000, 20, 0, False),              # read-free buffers
+    (1_000_003, 5_000, 30, False),
+    (29_903, 60_000, 0, False),           # deep enough for the tiled kernel: plain pileup + summary
+])
+def test_pileup_summary_matches_separate_calls(ctx, L, n, mbq, show_n):
+    """bc_pileup_summary (numpy's buffer partials computed inside the sparse sweep) gives the
+    same per-position outputs and the same summary doubles, bit for bit, as bc_pileup followed
+    by bc_summary, and the summary equals numpy's mean over the arrays (main.py:469-499)."""
+    rng = np.random.default_rng(L + n)
+    b = random_batch(rng, L, n)
+    k = 6 if show_n else 5
+    nf, nf2 = norm_factors(k)
+    r = D.DeviceReads(ctx, b)
+    outs = []
+    for fused in (False, True):
+        bufs = [ctx.alloc(max(8, x)) for x in (4 * k * L, 4 * L, 8 * L, 8 * L)]
+        work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        work.zero()
+        if fused:
+            ctx.pileup_summary(r, L, mbq, k, nf, nf2, bufs[0].ptr, bufs[1].ptr, None, bufs[2].ptr,
+                               bufs[3].ptr, work.ptr, dout.ptr)
+        else:
+            ctx.pileup(r, L, mbq, k, nf, nf2, bufs[0].ptr, bufs[1].ptr, None, bufs[2].ptr, bufs[3].ptr)
+            ctx.summary(bufs[1].ptr, bufs[2].ptr, L, work.ptr, dout.ptr)
+        assert ctx.range_error() == -1
+        outs.append((bufs[0].download(np.int32, k * L), bufs[1].download(np.int32, L),
+                     bufs[2].download(np.float64, L), bufs[3].download(np.float64, L),
+                     dout.download(np.float64, 4)))
+    for a, b2 in zip(*outs):
+        assert np.array_equal(a, b2)
+    cov, ent, s = outs[1][1], outs[1][2], outs[1][4]
+    assert s[0] == np.mean(cov.astype(np.int64)) and s[1] == np.mean(ent)
+    assert int(s[2]) == int(np.count_nonzero(cov)) and int(s[3]) == int(cov.astype(np.int64).sum())
+
+
+def test_summary_fold_many_references(ctx):
+    """bc_pileup_partials on 30 references, then ONE bc_summary_fold (two launches of up to 24
+    side-by-side folds): each reference's 4 doubles equal bc_pileup + bc_summary's."""
+    rng = np.random.default_rng(77)
+    k = 5
+    nf, nf2 = norm_factors(k)
+    keep, lens, works, outs, expect = [], [], [], [], []
+    for i in range(30):
+        L = int(rng.choice([700, 8192, 8192 * 3 + 11, 40_000, 150_000]))
+        b = random_batch(rng, L, int(rng.integers(50, 3000)))
+        r = D.DeviceReads(ctx, b)
+        bufs = [ctx.alloc(max(8, x)) for x in (4 * k * L, 4 * L, 8 * L, 8 * L)]
+        work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        ctx.pileup_partials(r, L, 0, k, nf, nf2, bufs[0].ptr, bufs[1].ptr, None, bufs[2].ptr,
+                            bufs[3].ptr, work.ptr)
+        keep.append((r, bufs, work, dout))
+        lens.append(L)
+        works.append(work.ptr)
+        outs.append(dout.ptr)
+        w2, d2 = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        ctx.summary(bufs[1].ptr, bufs[2].ptr, L, w2.ptr, d2.ptr)
+        expect.append(d2.download(np.float64, 4))
+    ctx.summary_fold(lens, works, outs)
+    assert ctx.range_error() == -1
+    for (r, bufs, work, dout), e in zip(keep, expect):
+        assert np.array_equal(dout.download(np.float64, 4), e)

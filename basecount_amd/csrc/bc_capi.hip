@@ -477,10 +477,8 @@ int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, in
                                         d_pc, d_ent, d_sec, c->d_err, c->shape, c->tile_waves, &parts));
     }
     const int64_t first = parts.fused ? parts.full_chunks : 0;
-    if (first < (L + 8191) / 8192) {  // the last, partial buffer (or all of them)
-        Timed tm(c, BC_K_SUMMARY);
-        HIP_TRY(bc::launch_summary_partials(c->stream, d_cov, d_ent, L, d_work, first));
-    }
+    Timed tm(c, BC_K_SUMMARY);  // the last, partial buffer (or all of them), and the header
+    HIP_TRY(bc::launch_summary_partials(c->stream, d_cov, d_ent, L, d_work, first));
     return BC_OK;
 }
 

@@ -63,11 +63,15 @@ hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, do
 // Summary partials (the per-8192-buffer sums bc_summary starts from): when the sparse sweep
 // runs with `parts`, it writes those of the whole buffers [0, full_chunks) itself (fused = true).
 struct SumParts {
-    double* ent;
+    int32_t* hdr;  // the work buffer's header: [0] = buffers whose partials are the quarters'
+    double* ent;  // per buffer
     long long* cov;
     long long* nz;
+    double* sub_ent;  // per quarter buffer (2048 positions), written by the sparse sweep
+    long long* sub_cov;
+    long long* sub_nz;
     bool fused;
-    int64_t full_chunks;
+    int64_t full_chunks;  // buffers whose partials are in the quarter arrays (fused)
 };
 // shape: BC_SHAPE_*; tile_waves: 0 = from the depth, else 1/2/4/8 waves per tile
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
@@ -86,6 +90,7 @@ hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, 
                           double* out, int64_t first_chunk = 0);
 hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
                                    int64_t first_chunk);
+// (the work buffers' headers say which leading buffers come as quarters)
 hipError_t launch_summary_fold(hipStream_t s, int n, const int64_t* L, void* const* work, double* const* out);
 // the partial arrays inside a summary work buffer
 SumParts summary_parts(void* work, int64_t L);

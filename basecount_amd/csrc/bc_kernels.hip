@@ -534,6 +534,10 @@ struct FoldRef {
     const double* pe;
     const long long* pc;
     const long long* pn;
+    const double* qe;  // quarter partials of the buffers [0, *nquart)
+    const long long* qc;
+    const long long* qn;
+    const int32_t* nquart;  // the work buffer's header (set by whoever produced the partials)
     int64_t nchunks;
     int64_t L;
     double* out;
@@ -552,6 +556,7 @@ __global__ __launch_bounds__(256) void k_sum_final(FoldArgs FA) {
     const long long* part_cov = R.pc;
     const long long* part_nz = R.pn;
     const int64_t nchunks = R.nchunks;
+    const int64_t nq = *R.nquart;
     const int t = threadIdx.x;
     double s = 0.0;
     long long cs = 0, nz = 0;
@@ -561,10 +566,17 @@ __global__ __launch_bounds__(256) void k_sum_final(FoldArgs FA) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int64_t c = r0 + t + 256 * j;
-            const bool in = c < nchunks;
-            v[j] = in ? part_ent[c] : 0.0;
-            vc[j] = in ? part_cov[c] : 0;
-            vn[j] = in ? part_nz[c] : 0;
+            if (c < nq) {  // a buffer's 4 quarters: (q0 + q1) + (q2 + q3), numpy's tree
+                const double* q = R.qe + 4 * c;
+                v[j] = (q[0] + q[1]) + (q[2] + q[3]);
+                vc[j] = (R.qc[4 * c] + R.qc[4 * c + 1]) + (R.qc[4 * c + 2] + R.qc[4 * c + 3]);
+                vn[j] = (R.qn[4 * c] + R.qn[4 * c + 1]) + (R.qn[4 * c + 2] + R.qn[4 * c + 3]);
+            } else {
+                const bool in = c < nchunks;
+                v[j] = in ? part_ent[c] : 0.0;
+                vc[j] = in ? part_cov[c] : 0;
+                vn[j] = in ? part_nz[c] : 0;
+            }
         }
     };
     auto stash = [&](int buf) {
@@ -781,15 +793,20 @@ hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, do
 
 size_t summary_work_bytes(int64_t L) {
     const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
-    return (size_t)(nc > 0 ? nc : 1) * 24;
+    return 16 + (size_t)(nc > 0 ? nc : 1) * 24 * 5;  // header; per buffer: its partials + its 4 quarters'
 }
 
 SumParts summary_parts(void* work, int64_t L) {
     const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
+    const int64_t m = nc > 0 ? nc : 1;
     SumParts P;
-    P.ent = (double*)work;
-    P.cov = (long long*)(P.ent + (nc > 0 ? nc : 1));
-    P.nz = P.cov + (nc > 0 ? nc : 1);
+    P.hdr = (int32_t*)work;  // [0]: buffers whose partials are in the quarter arrays
+    P.ent = (double*)((uint8_t*)work + 16);
+    P.cov = (long long*)(P.ent + m);
+    P.nz = P.cov + m;
+    P.sub_ent = (double*)(P.nz + m);
+    P.sub_cov = (long long*)(P.sub_ent + 4 * m);
+    P.sub_nz = P.sub_cov + 4 * m;
     P.fused = false;
     P.full_chunks = 0;
     return P;
@@ -801,6 +818,9 @@ hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const doub
                                    int64_t first_chunk) {
     const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
     const SumParts P = summary_parts(work, L);
+    // the header tells the fold how many leading buffers come as quarters (stream-ordered)
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)P.hdr, (int)first_chunk, 1, s);
+    if (e != hipSuccess) return e;
     if (nc > first_chunk)
         hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)(nc - first_chunk)), dim3(256), 0, s, cov, ent, L, P.ent, P.cov,
                            P.nz, first_chunk);
@@ -814,7 +834,8 @@ hipError_t launch_summary_fold(hipStream_t s, int n, const int64_t* L, void* con
         const int m = n - i0 < kFoldMax ? n - i0 : kFoldMax;
         for (int i = 0; i < m; ++i) {
             const SumParts P = summary_parts(work[i0 + i], L[i0 + i]);
-            FA.ref[i] = FoldRef{P.ent, P.cov, P.nz, (L[i0 + i] + kNpBuf - 1) / kNpBuf, L[i0 + i], out[i0 + i]};
+            FA.ref[i] = FoldRef{P.ent,    P.cov,  P.nz, P.sub_ent, P.sub_cov, P.sub_nz,
+                                P.hdr,    (L[i0 + i] + kNpBuf - 1) / kNpBuf, L[i0 + i], out[i0 + i]};
         }
         hipLaunchKernelGGL(k_sum_final, dim3((unsigned)m), dim3(256), 0, s, FA);
     }

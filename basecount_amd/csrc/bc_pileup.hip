@@ -60,11 +60,12 @@ struct PileArgs {
     int64_t seq_words;   // readable 32-bit words of seq (bc_seq_event_bytes / 4)
     int64_t qual_bytes;
     int64_t tiles_per_wave;  // k_pileup_solo: consecutive tiles swept by one wave
-    // k_pileup_solo with summary partials (bc_pileup_summary): numpy's per-8192-buffer pairwise
-    // entropy sums and the exact coverage / non-zero sums of the buffers [0, full_chunks)
-    double* part_ent;
-    long long* part_cov;
-    long long* part_nz;
+    // k_pileup_solo with summary partials (bc_pileup_partials): for every quarter (2048
+    // positions, a subtree of numpy's pairwise tree) of the whole buffers [0, full_chunks), its
+    // pairwise entropy sum and exact coverage / non-zero sums
+    double* sub_ent;
+    long long* sub_cov;
+    long long* sub_nz;
     int64_t full_chunks;
     int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 4 no walk, 8 no stats
                  // math, 16 no stores, 32 no sequence staging
@@ -703,30 +704,38 @@ __device__ __forceinline__ double pos_stats(const PileArgs& A, const uint32_t* c
 
 // numpy's pairwise_sum of one 128-element leaf (pw_leaf of bc_kernels.hip for n = 128) from two
 // consecutive tiles' entropies, one per lane: r_j = a[j] + a[8 + j] + ... + a[120 + j] in that
-// order (eight accumulators), then ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)).  The first
-// tile's half of the chains (leaf_half) is taken when that tile is done, so only its 8
-// accumulators stay live; leaf_finish adds the second tile's values and combines.  Every lane
-// returns the leaf.
-__device__ __forceinline__ double leaf_half(double ea, int lane) {
+// order (eight accumulators), then ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)).  A tile's 64
+// values go through the wave's LDS scratch `tr` (one store, then lanes 0-7 read their 8 strided
+// values): leaf_half takes the first tile's half of the chains, leaf_finish the second's and the
+// combine.  The leaf is valid in lane 0.
+__device__ __forceinline__ double leaf_half(double ea, int lane, double* tr) {
+    tr[lane] = ea;
+    __builtin_amdgcn_wave_barrier();
     const int j = lane & 7;
     double v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = __shfl(ea, 8 * i + j);
+    for (int i = 0; i < 8; ++i) v[i] = tr[8 * i + j];
     double r = v[0];
 #pragma unroll
     for (int i = 1; i < 8; ++i) r = r + v[i];
+    __builtin_amdgcn_wave_barrier();
     return r;
 }
-__device__ __forceinline__ double leaf_finish(double r, double eb, int lane) {
+__device__ __forceinline__ double leaf_finish(double r, double eb, int lane, double* tr) {
+    tr[lane] = eb;
+    __builtin_amdgcn_wave_barrier();
     const int j = lane & 7;
     double v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = __shfl(eb, 8 * i + j);
+    for (int i = 0; i < 8; ++i) v[i] = tr[8 * i + j];
 #pragma unroll
     for (int i = 0; i < 8; ++i) r = r + v[i];
-    const double r01 = r + __shfl(r, j + 1);      // lanes 0, 2, 4, 6: r_j + r_j+1
-    const double r03 = r01 + __shfl(r01, j + 2);  // lanes 0, 4
-    return __shfl(r03, 0) + __shfl(r03, 4);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 8) tr[lane] = r;
+    __builtin_amdgcn_wave_barrier();
+    const double leaf = ((tr[0] + tr[1]) + (tr[2] + tr[3])) + ((tr[4] + tr[5]) + (tr[6] + tr[7]));
+    __builtin_amdgcn_wave_barrier();
+    return leaf;
 }
 
 __device__ __forceinline__ long long wave_sum_i64(long long v) {
@@ -779,12 +788,14 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     int64_t wlo_base = lo, whi_base = hi;
     int32_t wlo = lo + lane < A.n ? A.pos[lo + lane] : INT32_MAX;
     int32_t whi = hi + lane < A.n ? A.pos[hi + lane] : INT32_MAX;
-    // SUMP: the wave's tiles start on a buffer boundary (tiles_per_wave is a multiple of 128), so
-    // it sees whole 8192-position buffers: leaves of two tiles, merged into the buffer's pairwise
-    // tree (numpy splits 8192 evenly down to 128): the leaves wait in LDS (64 per wave) and are
-    // added pairwise across the lanes once the buffer is complete
+    // SUMP: the wave's tiles start on a quarter-buffer boundary (tiles_per_wave is a multiple of
+    // 32), so it sees whole 2048-position quarters, each a subtree of numpy's pairwise tree over
+    // an 8192 buffer (split evenly down to 128-element leaves): leaves of two tiles wait in LDS (16
+    // per quarter) and are added pairwise across the lanes once the quarter is complete; the fold
+    // kernel joins the 4 quarters of a buffer
     double e_prev = 0.0;
-    double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + 64 * wave;
+    double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + 128 * wave;
+    double* mytr = myleaves + 64;  // transposition scratch of the leaf sums
     long long sum_cov = 0, sum_nz = 0;
     for (int64_t t = t_begin; t < t_end; ++t) {
         const int64_t t0 = t * kTile;
@@ -845,27 +856,28 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
                         sum_cov += cov;
                         sum_nz += cov != 0;
                         if (t & 1) {
-                            const double lf = leaf_finish(e_prev, h, lane);
-                            const int leaf = (int)((t >> 1) & 63);
+                            const double lf = leaf_finish(e_prev, h, lane, mytr);
+                            const int leaf = (int)((t >> 1) & 15);
                             if (lane == 0) myleaves[leaf] = lf;
-                            if (leaf == 63) {  // the buffer is complete: its 64 leaves, pairwise
+                            if (leaf == 15) {  // the quarter is complete: its 16 leaves, pairwise
                                 __builtin_amdgcn_wave_barrier();
-                                double v = myleaves[lane];
+                                double v = myleaves[lane & 15];
 #pragma unroll
-                                for (int l = 1; l < 64; l <<= 1) {  // left (lower lanes) + right
+                                for (int l = 1; l < 16; l <<= 1) {  // left (lower lanes) + right
                                     const double w = __shfl_down(v, l);
                                     if ((lane & (2 * l - 1)) == 0) v = v + w;
                                 }
                                 const long long cs = wave_sum_i64(sum_cov), nz = wave_sum_i64(sum_nz);
                                 if (lane == 0) {
-                                    A.part_ent[ch] = v;
-                                    A.part_cov[ch] = cs;
-                                    A.part_nz[ch] = nz;
+                                    const int64_t q = t >> 5;
+                                    A.sub_ent[q] = v;
+                                    A.sub_cov[q] = cs;
+                                    A.sub_nz[q] = nz;
                                 }
                                 sum_cov = sum_nz = 0;
                             }
                         } else {
-                            e_prev = leaf_half(h, lane);  // the first tile's half of the chains
+                            e_prev = leaf_half(h, lane, mytr);  // the first tile's half of the chains
                         }
                     }
                 }
@@ -930,11 +942,11 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         A.tiles_per_wave = (A.n_tiles + target_waves - 1) / target_waves;
         if (A.tiles_per_wave < 1) A.tiles_per_wave = 1;
         const bool sump = parts && stats && L >= kNpBuf;
-        if (sump) {  // whole 8192-position buffers per wave: the summary partials come for free
-            A.tiles_per_wave = (A.tiles_per_wave + 127) / 128 * 128;
-            A.part_ent = parts->ent;
-            A.part_cov = parts->cov;
-            A.part_nz = parts->nz;
+        if (sump) {  // whole quarter buffers per wave: the summary partials come for free
+            A.tiles_per_wave = (A.tiles_per_wave + 31) / 32 * 32;
+            A.sub_ent = parts->sub_ent;
+            A.sub_cov = parts->sub_cov;
+            A.sub_nz = parts->sub_nz;
             A.full_chunks = L / kNpBuf;
             parts->fused = true;
             parts->full_chunks = A.full_chunks;
@@ -943,7 +955,7 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         int64_t blocks = (waves + nw - 1) / nw;
         blocks = (blocks + 7) / 8 * 8;  // a multiple of the XCD count (see the kernel's tile mapping)
         const dim3 grid((unsigned)blocks), block(64 * nw);
-        const size_t lds = (size_t)nw * (kRecBytes + kStageRegion) + (sump ? (size_t)nw * 64 * 8 : 0);
+        const size_t lds = (size_t)nw * (kRecBytes + kStageRegion) + (sump ? (size_t)nw * 128 * 8 : 0);
 #define BC_SOLO(Q, KK, ST)                                                                   \
     do {                                                                                     \
         if (sump) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true>), grid, block, lds, s, A); \

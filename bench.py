@@ -194,7 +194,8 @@ def e2e_c2(rs) -> dict:
 class Workload:
     """One config's contigs for this rank, resident in HBM before anything is timed."""
 
-    def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool):
+    def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool,
+                 fused_summary: bool = True):
         from basecount_amd import device as D
         from basecount_amd import synth
         from basecount_amd.bam import seq_to_event
@@ -219,6 +220,7 @@ class Workload:
         self.k = 5
         self.want_pc = not self.per_contig  # c5 is only ever summarised: no percentages
         self.summarise = summarise
+        self.fused_summary = fused_summary
         self.nf, self.nf2 = norm_factors(self.k)
         self.work = []
         ev = None
@@ -242,13 +244,17 @@ class Workload:
         ctx = self.ctx
         for i, (_, L, _, reads, o) in enumerate(self.work):
             pc = o["pc"].ptr if o["pc"] is not None else None
-            if self.summarise:  # kernels 1 + 2 and the summary's per-buffer partial sums
+            if self.summarise and self.fused_summary:  # kernels 1 + 2 and the summary's partials
                 ctx.pileup_partials(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr,
                                     o["cov"].ptr, pc, o["ent"].ptr, o["sec"].ptr, o["swork"].ptr)
+            elif self.summarise:  # kernels 1 + 2, then bc_summary re-reading coverage / entropy
+                ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
+                           pc, o["ent"].ptr, o["sec"].ptr)
+                ctx.summary(o["cov"].ptr, o["ent"].ptr, L, o["swork"].ptr, self.d_sum.ptr + 32 * i)
             else:
                 ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
                            pc, o["ent"].ptr, o["sec"].ptr)
-        if self.summarise:  # every contig's sequential fold, side by side (bc_summary_fold)
+        if self.summarise and self.fused_summary:  # every contig's fold, side by side
             ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
                              [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
 
@@ -334,7 +340,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     max over ranks) and describe them."""
     from basecount_amd import device as D
 
-    wl = Workload(ctx, cfg, rank, world, args.mbq, summarise)
+    wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused")
     rccl = group is not None and getattr(group, "backend", "") == "rccl"
     gather = None
     if summarise and group is not None:
@@ -501,6 +507,9 @@ def main():
     ap.add_argument("--shape", default="auto", choices=["auto", "tile", "rc", "tile_no_solo"],
                     help="kernel shape override (bc_ctx_set_shape), recorded in the output")
     ap.add_argument("--tile-waves", type=int, default=0, help="waves per tile override (0 = auto)")
+    ap.add_argument("--summary-path", choices=["fused", "separate"], default="fused",
+                    help="c5: summary partials in the pileup sweep + one fold (fused), or bc_pileup "
+                         "then bc_summary per contig (separate)")
     ap.add_argument("--allow-diag", action="store_true",
                     help="run a diagnostic (BC_DIAG) build; its numbers are marked as such")
     args = ap.parse_args()
@@ -589,7 +598,8 @@ def main():
                        "percentages_stored": args.config != "c5",
                        "parallelism": f"contig-sharded x{world}",
                        "comm": (group.backend if group is not None else None),
-                       "shape": args.shape, "tile_waves": args.tile_waves, "build": build},
+                       "shape": args.shape, "tile_waves": args.tile_waves,
+                       "summary_path": args.summary_path, "build": build},
             "gbases_piled_per_s": head["gbases_piled_per_s"],
             "device_us_per_step": head["device_us_per_step"],
             "kernel_us": head["kernel_us"],

@@ -523,6 +523,54 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const do
     }
 }
 
+// The last, partial buffer of a reference (m < 8192 elements): numpy's generic pairwise tree
+// (pw_block) over the entropies staged in LDS, so the leaves are summed from LDS instead of one
+// dependent global load after another; every global load of the buffer is issued at once.
+__global__ __launch_bounds__(256) void k_sum_tail(const int32_t* cov, const double* ent, int64_t L,
+                                                  double* part_ent, long long* part_cov, long long* part_nz,
+                                                  int64_t chunk) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    double* s_ent = (double*)dyn;  // [m]
+    __shared__ long long s_red[8];
+    __shared__ int s_off[128], s_len[128];
+    __shared__ double s_val[128];
+    const int64_t c0 = chunk * kNpBuf;
+    const int m = (int)(L - c0);  // 0 < m < 8192
+    const int t = threadIdx.x;
+    int cv[32];
+    double ev[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const int i = t + 256 * j;
+        cv[j] = i < m ? cov[c0 + i] : 0;
+        ev[j] = i < m ? ent[c0 + i] : 0.0;
+    }
+    long long cs = 0, nz = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        cs += cv[j];
+        nz += cv[j] != 0;
+        const int i = t + 256 * j;
+        if (i < m) s_ent[i] = ev[j];
+    }
+    __syncthreads();
+    const double e = pw_block(s_ent, m, s_off, s_len, s_val);
+    for (int o = 32; o > 0; o >>= 1) {
+        cs += __shfl_down(cs, o);
+        nz += __shfl_down(nz, o);
+    }
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = cs;
+        s_red[4 + (t >> 6)] = nz;
+    }
+    __syncthreads();
+    if (t == 0) {
+        part_ent[chunk] = e;
+        part_cov[chunk] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        part_nz[chunk] = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
+    }
+}
+
 // The float64 fold over the per-buffer partials stays sequential (numpy adds the buffers'
 // pairwise sums in order: one dependent add per buffer is the floor).  One workgroup per
 // reference, so the folds of several references (bc_summary_fold) run side by side.  The
@@ -821,9 +869,13 @@ hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const doub
     // the header tells the fold how many leading buffers come as quarters (stream-ordered)
     hipError_t e = hipMemsetD32Async((hipDeviceptr_t)P.hdr, (int)first_chunk, 1, s);
     if (e != hipSuccess) return e;
-    if (nc > first_chunk)
-        hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)(nc - first_chunk)), dim3(256), 0, s, cov, ent, L, P.ent, P.cov,
-                           P.nz, first_chunk);
+    const int64_t nfull = L / kNpBuf;  // whole buffers: k_sum_chunks; the partial one: k_sum_tail
+    if (nfull > first_chunk)
+        hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)(nfull - first_chunk)), dim3(256), 0, s, cov, ent, L, P.ent,
+                           P.cov, P.nz, first_chunk);
+    if (nc > nfull && nfull >= first_chunk)
+        hipLaunchKernelGGL(k_sum_tail, dim3(1), dim3(256), (size_t)(L - nfull * kNpBuf) * sizeof(double), s, cov, ent,
+                           L, P.ent, P.cov, P.nz, nfull);
     return hipGetLastError();
 }
 

@@ -228,6 +228,8 @@ class Workload:
             b = synth.batch_arrays(self.rs, t, 0)
             if ev is None:  # the read set's SEQ in the kernels' layout, built once on the host
                 ev = seq_to_event(b["seq"])
+            if mbq == 0:  # qualities are never read without a threshold: not uploaded
+                b = dict(b, qual=None)
             reads = D.DeviceReads(ctx, dict(b, seq_event=ev))
             assert reads.r.sorted == 1
             k = self.k

@@ -142,3 +142,28 @@ def test_c3_cli_rows(c3_bam):
                             "num_ds", "pc_a", "pc_c", "pc_g", "pc_t", "pc_ds", "entropy",
                             "secondary_entropy"]) + "\n"
         assert got == header + O.rows_text(f.references[0], exp, False, False, 3)
+
+
+def test_unsorted_bam_cli_rows(tmp_path):
+    """An unsorted BAM (C2 shape, 3 contigs, reads in random order): the CLI takes the
+    event-parallel k_count + k_stats path; rows byte-identical to the oracle's main.py:454-466."""
+    rs = synth.make_reads([("u1", 29_903), ("u2", 5_000), ("u3", 70_000)], 40_000, True, 91, unsorted=True)
+    order = np.random.default_rng(5).permutation(rs.n)  # interleave the contigs too
+    rs2 = synth.ReadSet(references=rs.references, lengths=rs.lengths, tid=rs.tid[order], pos=rs.pos[order],
+                        flag=rs.flag[order], mapq=rs.mapq[order],
+                        cig_off=np.concatenate([[0], np.cumsum(np.diff(rs.cig_off)[order])]).astype(np.uint64),
+                        cigar=np.concatenate([rs.cigar[int(rs.cig_off[i]):int(rs.cig_off[i + 1])] for i in order]),
+                        l_seq=rs.l_seq[order], seq_off=rs.seq_off,
+                        seq=rs.seq.reshape(rs.n, -1)[order].reshape(-1), qual_off=rs.qual_off,
+                        qual=rs.qual.reshape(rs.n, -1)[order].reshape(-1), qstart=rs.qstart[order])
+    bam = str(tmp_path / "unsorted.bam")
+    synth.write_bam(rs2, bam)
+    got = _run_cli([bam, "--show-n-bases", "--min-base-quality", "15"])
+    header, blocks = O.split_blocks(got, False)
+    with BamFile(bam) as f:
+        assert sorted(blocks) == sorted(f.references)
+        for t, name in enumerate(f.references):
+            b, _ = O.batch_from_bam(f, t, 0)
+            exp, (br, _) = O.bcount(f.lengths[t], 15, b)
+            assert br == -1
+            assert blocks[name] == O.rows_text(name, exp, True, False, 3), name

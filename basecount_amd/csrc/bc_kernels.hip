@@ -357,78 +357,58 @@ __device__ double pw_leaf(const double* a, int n) {
     return res;
 }
 
-// Generic pairwise sum of a[0..m), m <= 8192, by one workgroup (any blockDim >= 128).
-// Thread 0 enumerates the leaves of numpy's recursion (<= 128 of them), the block sums the
-// leaves in parallel, thread 0 folds them back in the recursion's order.  Returns the value in
-// thread 0 only.
+// Generic pairwise sum of a[0..m), m <= 8192, by one workgroup (any blockDim >= 128).  numpy's
+// recursion (split at n2 = n/2 - (n/2)%8 down to leaves of <= 128) is laid out level by level in
+// LDS, in parallel: node i of level l has children 2i, 2i+1 of level l+1; a leaf passes itself
+// down as its left child (and an empty right one), so level kLv holds every leaf in order.  The
+// leaves are summed in parallel, then every level adds its children bottom-up: the same sums in
+// the same order as the recursion, with no per-thread stack (a private array there lives in
+// scratch memory, one slow round trip per push).  Returns the value in thread 0 only.
+constexpr int kLv = 7;  // 8192 -> 4096 -> ... -> 128: six splits; one spare level
 __device__ double pw_block(const double* a, int m, int* s_off, int* s_len, double* s_val) {
-    __shared__ int s_nleaf;
-    if (threadIdx.x == 0) {
-        int stk_o[32], stk_l[32], sp = 0, nl = 0;
-        stk_o[sp] = 0;
-        stk_l[sp++] = m;
-        while (sp) {
-            const int o = stk_o[--sp], l = stk_l[sp];
-            if (l <= 128) {
-                s_off[nl] = o;
-                s_len[nl++] = l;
-            } else {
-                int n2 = l / 2;
-                n2 -= n2 % 8;
-                stk_o[sp] = o + n2;  // right first so left pops first
-                stk_l[sp++] = l - n2;
-                stk_o[sp] = o;
-                stk_l[sp++] = n2;
-            }
-        }
-        s_nleaf = nl;
+    // s_off / s_len: (2^(kLv+1) - 1) nodes; s_val: 2 x 2^kLv values (ping-pong)
+    const int t = threadIdx.x;
+    if (t == 0) {
+        s_off[0] = 0;
+        s_len[0] = m;
     }
     __syncthreads();
-    const int nl = s_nleaf;
-    for (int t = threadIdx.x; t < nl; t += blockDim.x) s_val[t] = pw_leaf(a + s_off[t], s_len[t]);
-    __syncthreads();
-    double result = 0.0;
-    if (threadIdx.x == 0) {
-        // evaluate pw(m) recursively with an explicit stack; leaves consumed left to right
-        int st_len[32], st_stage[32];
-        double st_acc[32];
-        int sp = 0, leaf = 0;
-        st_len[0] = m;
-        st_stage[0] = 0;
-        sp = 1;
-        double ret = 0.0;
-        while (sp) {
-            const int top = sp - 1;
-            const int l = st_len[top];
-            if (l <= 128) {
-                ret = s_val[leaf++];
-                --sp;
-            } else {
-                int n2 = l / 2;
+    for (int l = 0; l < kLv; ++l) {  // top-down: split the nodes of level l
+        const int base = (1 << l) - 1, nb = (1 << (l + 1)) - 1;
+        for (int i = t; i < (1 << l); i += blockDim.x) {
+            const int o = s_off[base + i], n = s_len[base + i];
+            int n2 = n;
+            if (n > 128) {
+                n2 = n / 2;
                 n2 -= n2 % 8;
-                if (st_stage[top] == 0) {
-                    st_stage[top] = 1;
-                    st_len[sp] = n2;
-                    st_stage[sp] = 0;
-                    ++sp;
-                    continue;
-                } else if (st_stage[top] == 1) {
-                    st_acc[top] = ret;
-                    st_stage[top] = 2;
-                    st_len[sp] = l - n2;
-                    st_stage[sp] = 0;
-                    ++sp;
-                    continue;
-                } else {
-                    ret = st_acc[top] + ret;
-                    --sp;
-                }
             }
+            s_off[nb + 2 * i] = o;
+            s_len[nb + 2 * i] = n2;
+            s_off[nb + 2 * i + 1] = o + n2;
+            s_len[nb + 2 * i + 1] = n - n2;
         }
-        result = ret;
+        __syncthreads();
+    }
+    const int leaves = 1 << kLv, lbase = leaves - 1;
+    double* cur = s_val;
+    double* nxt = s_val + leaves;
+    for (int i = t; i < leaves; i += blockDim.x) {
+        const int n = s_len[lbase + i];
+        cur[i] = n > 0 ? pw_leaf(a + s_off[lbase + i], n) : 0.0;
     }
     __syncthreads();
-    return result;
+    for (int l = kLv - 1; l >= 0; --l) {  // bottom-up: a split node adds its children, left + right
+        const int base = (1 << l) - 1;
+        for (int i = t; i < (1 << l); i += blockDim.x)
+            nxt[i] = s_len[base + i] > 128 ? cur[2 * i] + cur[2 * i + 1] : cur[2 * i];
+        __syncthreads();
+        double* tmp = cur;
+        cur = nxt;
+        nxt = tmp;
+    }
+    const double r = t == 0 ? cur[0] : 0.0;
+    __syncthreads();
+    return r;
 }
 
 // Full 8192-element buffer with the fixed tree: 64 leaves of 128; 256 threads, thread t owns
@@ -479,8 +459,8 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const do
                                                     int64_t first_chunk) {
     __shared__ double s_wave[4];
     __shared__ long long s_red[8];
-    __shared__ int s_off[128], s_len[128];
-    __shared__ double s_val[128];
+    __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
+    __shared__ double s_val[2 << kLv];
     const int64_t chunk = first_chunk + blockIdx.x;
     const int64_t c0 = chunk * kNpBuf;
     const int m = (int)((L - c0) < kNpBuf ? (L - c0) : kNpBuf);
@@ -532,8 +512,8 @@ __global__ __launch_bounds__(256) void k_sum_tail(const int32_t* cov, const doub
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     double* s_ent = (double*)dyn;  // [m]
     __shared__ long long s_red[8];
-    __shared__ int s_off[128], s_len[128];
-    __shared__ double s_val[128];
+    __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
+    __shared__ double s_val[2 << kLv];
     const int64_t c0 = chunk * kNpBuf;
     const int m = (int)(L - c0);  // 0 < m < 8192
     const int t = threadIdx.x;
@@ -729,8 +709,8 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
     __shared__ unsigned s_hist[256];
     __shared__ unsigned long long s_sel[2];
     __shared__ long long s_red[4];
-    __shared__ int s_off[128], s_len[128];
-    __shared__ double s_val[128];
+    __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
+    __shared__ double s_val[2 << kLv];
     const int t = blockIdx.x;
     int64_t lo = lo_a[t], hi = hi_a[t];
     if (lo < 0) lo = 0;

@@ -685,12 +685,37 @@ def run(argv=None):
     from . import dist
 
     group = dist.Group() if dist.env()[0] > 1 else None  # RCCL (default) or gloo, DESIGN.md §6
+    timing = os.environ.get("BASECOUNT_HIP_TIMING") not in (None, "", "0")
+    t0 = None
+    if timing:  # per-kernel device times and the wall time on stderr; stdout unchanged
+        import time
+
+        t0 = time.perf_counter()
+        context().timing(True)
     try:
         _run(args, references, min_base_quality, min_mapping_quality, chunk_size, bed,
              decimal_places, group)
     finally:
         if group is not None:
             group.close()
+        if timing:
+            _timing_report(time.perf_counter() - t0)
+
+
+def _timing_report(wall_s: float) -> None:
+    """BASECOUNT_HIP_TIMING=1: one stderr line per kernel id (launches, mean device time) and the
+    run's wall time."""
+    import sys
+
+    try:
+        rep = context().timing_report()
+    except Exception as e:  # noqa: BLE001 - reporting must not mask the run's own outcome
+        rep = {"error": str(e)}
+    rank = os.environ.get("RANK", "0")
+    for name, v in sorted(rep.items()):
+        if isinstance(v, tuple):
+            print(f"basecount[{rank}] kernel {name}: {v[0]} launches, {v[1]:.2f} us mean", file=sys.stderr)
+    print(f"basecount[{rank}] wall {wall_s * 1e3:.2f} ms", file=sys.stderr)
 
 
 def _run(args, references, min_base_quality, min_mapping_quality, chunk_size, bed, dp, group):

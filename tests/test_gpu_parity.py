@@ -532,3 +532,17 @@ def test_summary_fold_many_references(ctx):
     assert ctx.range_error() == -1
     for (r, bufs, work, dout), e in zip(keep, expect):
         assert np.array_equal(dout.download(np.float64, 4), e)
+
+
+def test_cli_timing_report_keeps_stdout(golden, manifest, tmp_path):
+    """BASECOUNT_HIP_TIMING=1: kernel times and the wall time on stderr, stdout still
+    byte-identical to the reference's."""
+    c = manifest["c1_default"]
+    env = dict(os.environ, PYTHONPATH=REPO, PYTHONHASHSEED="0", BASECOUNT_HIP_TIMING="1")
+    p = subprocess.run([sys.executable, "-m", "basecount_amd", c["bam"]] + c["args"], cwd=golden,
+                       env=env, capture_output=True, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    with open(os.path.join(golden, c["stdout"]), "rb") as fh:
+        assert p.stdout == gzip.decompress(fh.read())
+    err = p.stderr.decode()
+    assert "kernel pileup" in err and " launches, " in err and "wall " in err

@@ -14,15 +14,18 @@
 //
 // Domain: 0 < x < inf, the only inputs the entropies use (p = c / cov with 0 < c <= cov).
 #pragma once
-#include <hip/hip_runtime.h>
-
 #include <cstdint>
 
 #include "bc_log2_table.h"
 
+// device code by default; a host build (tests/log2_check.cpp) defines BC_LOG2_HD first
+#ifndef BC_LOG2_HD
+#define BC_LOG2_HD __device__ __forceinline__
+#endif
+
 namespace bc {
 
-__device__ __forceinline__ double glibc_log2(double x) {
+BC_LOG2_HD double glibc_log2(double x) {
     using namespace log2d;
     const uint64_t ix = __builtin_bit_cast(uint64_t, x);
     if (ix - 0x3feea4af00000000ull < 0x3ff0b55900000000ull - 0x3feea4af00000000ull) {

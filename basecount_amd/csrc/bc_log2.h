@@ -18,7 +18,7 @@
 
 #include "bc_log2_table.h"
 
-// device code by default; a host build (tests/log2_check.cpp) defines BC_LOG2_HD first
+// device code by default; a host build (tests/native/log2_check.cpp) defines BC_LOG2_HD first
 #ifndef BC_LOG2_HD
 #define BC_LOG2_HD __device__ __forceinline__
 #endif

@@ -92,6 +92,26 @@ std::pair<int, int64_t> host_spans(const bc_reads& r) {
     return {(int)std::min<uint64_t>(best, 0x7fffffff), end};
 }
 
+// bc_reads.tile_reads for a sorted batch with fewer 64-position tiles (up to max_end) than
+// reads / 16 and fewer than 2^31 reads, else empty: per tile t, [lo, hi) = the reads with
+// 64t - max_span < pos < 64t + 64, the range the tiled kernel otherwise searches for
+// (lower_bound_pair in bc_pileup.hip).  Two monotone cursors: O(reads + tiles).
+std::vector<int32_t> tile_index(const bc_reads& h, int sorted, int max_span, int64_t max_end) {
+    std::vector<int32_t> out;
+    const int64_t n = h.n_reads, tiles = (max_end + 63) / 64;
+    if (!sorted || n <= 0 || n >= (int64_t)0x7FFFFFC0 || tiles <= 0 || tiles > n / 16) return out;
+    out.resize((size_t)tiles * 2);
+    int64_t lo = 0, hi = 0;
+    for (int64_t t = 0; t < tiles; ++t) {
+        const int64_t vlo = 64 * t - max_span + 1, vhi = 64 * t + 64;
+        while (lo < n && (int64_t)h.pos[lo] < vlo) ++lo;
+        while (hi < n && (int64_t)h.pos[hi] < vhi) ++hi;
+        out[2 * t] = (int32_t)lo;
+        out[2 * t + 1] = (int32_t)hi;
+    }
+    return out;
+}
+
 int check_host_reads(const bc_reads* r) {
     if (!r) return fail(BC_E_ARG, "reads is NULL");
     if (r->n_reads < 0) return fail(BC_E_ARG, "n_reads < 0");
@@ -317,25 +337,30 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     // conversion pass; BC_SEQ_BAM is converted in place by k_seq_event after the copy
     const bool host_event = h->seq_layout == BC_SEQ_EVENT;
     const size_t n = (size_t)h->n_reads;
-    void* p[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // the tile index of a dense sorted batch (bc_reads.tile_reads): the read range of every
+    // 64-position tile, so the tiled kernel starts each tile with one load instead of a search
+    std::vector<int32_t> tidx = tile_index(*h, d->sorted, d->max_span, d->max_end);
+    constexpr int kArr = 8;
+    void* p[kArr] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // the sequence buffer is sized for BC_SEQ_EVENT (converted in place after the copy)
-    const size_t sz[7] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4, bc::seq_event_bytes(h->seq_bytes),
-                          h->qual ? (size_t)h->qual_bytes : 0};
-    const size_t cp[7] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6]};
-    const void* src[7] = {h->pos, h->cig_beg, h->cig_n, h->seq_nib, h->cigar, h->seq, h->qual};
+    const size_t sz[kArr] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4,
+                             bc::seq_event_bytes(h->seq_bytes), h->qual ? (size_t)h->qual_bytes : 0,
+                             tidx.size() * 4};
+    const size_t cp[kArr] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6], sz[7]};
+    const void* src[kArr] = {h->pos, h->cig_beg, h->cig_n, h->seq_nib, h->cigar, h->seq, h->qual, tidx.data()};
     // ONE slab for the whole batch (arrays 4 KiB-aligned inside it, the slab a multiple of 2 MiB):
     // the kernels' first touches of a batch then miss the GPU TLB on a few large fragments
     // instead of on every small buffer's pages.  The first array present is the slab base
     // (bc_reads_free).
-    size_t off[7], total = 0;
-    for (int i = 0; i < 7; ++i) {
+    size_t off[kArr], total = 0;
+    for (int i = 0; i < kArr; ++i) {
         off[i] = total;
         total += (sz[i] + 4095) / 4096 * 4096;
     }
     total = (total + (2u << 20) - 1) / (2u << 20) * (2u << 20);
     void* slab = nullptr;
     HIP_TRY(hipMalloc(&slab, total));
-    for (int i = 0; i < 7; ++i) {
+    for (int i = 0; i < kArr; ++i) {
         if (!sz[i]) continue;
         p[i] = (uint8_t*)slab + off[i];
         hipError_t e = cp[i] ? hipMemcpyAsync(p[i], src[i], cp[i], hipMemcpyHostToDevice, c->stream) : hipSuccess;
@@ -358,8 +383,10 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     d->cigar = (const uint32_t*)p[4];
     d->seq = (const uint8_t*)p[5];
     d->qual = (const uint8_t*)p[6];
+    d->tile_reads = (const int32_t*)p[7];
+    d->n_tiles = (int64_t)tidx.size() / 2;
     d->seq_layout = BC_SEQ_EVENT;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // also keeps tidx alive until its copy is done
     return BC_OK;
 }
 
@@ -367,7 +394,7 @@ int bc_reads_free(bc_ctx* c, bc_reads* d) {
     if (!c || !d) return fail(BC_E_ARG, "NULL argument");
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
-    const void* p[7] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual};
+    const void* p[8] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual, d->tile_reads};
     for (auto q : p)  // the first array present is the base of the batch's slab (bc_reads_upload)
         if (q) {
             (void)hipFree((void*)q);

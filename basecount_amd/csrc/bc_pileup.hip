@@ -2,7 +2,7 @@
 //
 // Layout: the reference is cut into 64-position tiles; a tile is owned by a group of S waves.
 // Reads are coordinate-sorted, so the reads overlapping a tile form one contiguous index range,
-// found in-kernel by a 64-ary search over pos[].  They are processed in chunks of 64: each lane
+// read from the batch's tile index (bc_reads.tile_reads) or found by a 64-ary search over pos[].  They are processed in chunks of 64: each lane
 // loads one read and decodes its CIGAR into a run table (count.cpp:40-96 semantics), the chunk's
 // packed sequence is staged into LDS, and then the chunk is walked with
 //     lane = (window g = lane >> 3, read slot s = lane & 7):
@@ -57,6 +57,8 @@ struct PileArgs {
     double* ent;
     double* sec;
     unsigned long long* err;
+    const int2* trange;  // bc_reads.tile_reads: [lo, hi) per tile t < n_trange, else searched
+    int64_t n_trange;
     int64_t seq_words;   // readable 32-bit words of seq (bc_seq_event_bytes / 4)
     int64_t qual_bytes;
     int64_t tiles_per_wave;  // k_pileup_solo: consecutive tiles swept by one wave
@@ -531,7 +533,13 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                 trace_stamp(A, 11);
             }
 #endif
-            lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
+            if (t < A.n_trange) {  // the upload's tile index: one load instead of a search
+                const int2 rg = A.trange[t];
+                lo = rg.x;
+                hi = rg.y;
+            } else {
+                lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
+            }
             trace_stamp(A, 9);
         }
         if (S > 1) {
@@ -899,6 +907,10 @@ PileArgs make_args(const bc_reads& r, int64_t L, uint32_t mbq) {
     A.n = r.n_reads;
     A.L = L;
     A.max_span = r.max_span;
+    if (r.tile_reads && r.n_tiles > 0 && !((uintptr_t)r.tile_reads & 7u)) {
+        A.trange = (const int2*)r.tile_reads;
+        A.n_trange = r.n_tiles;
+    }
     A.mbq = mbq;
     A.seq_words = (int64_t)(seq_event_bytes(r.seq_bytes) / 4);
     A.qual_bytes = r.qual ? r.qual_bytes : 0;

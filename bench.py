@@ -195,7 +195,7 @@ class Workload:
     """One config's contigs for this rank, resident in HBM before anything is timed."""
 
     def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool,
-                 fused_summary: bool = True):
+                 fused_summary: bool = True, tile_index: bool = True):
         from basecount_amd import device as D
         from basecount_amd import synth
         from basecount_amd.bam import seq_to_event
@@ -232,6 +232,9 @@ class Workload:
                 b = dict(b, qual=None)
             reads = D.DeviceReads(ctx, dict(b, seq_event=ev))
             assert reads.r.sorted == 1
+            if not tile_index:  # A/B: the tiled kernel searches pos[] (the index stays allocated)
+                reads.r.tile_reads = None
+                reads.r.n_tiles = 0
             k = self.k
             bufs = dict(counts=ctx.alloc(4 * k * L), cov=ctx.alloc(4 * L),
                         pc=ctx.alloc(8 * k * L) if self.want_pc else None, ent=ctx.alloc(8 * L),
@@ -342,7 +345,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     max over ranks) and describe them."""
     from basecount_amd import device as D
 
-    wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused")
+    wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused",
+                  args.tile_index == "on")
     rccl = group is not None and getattr(group, "backend", "") == "rccl"
     gather = None
     if summarise and group is not None:
@@ -512,6 +516,8 @@ def main():
     ap.add_argument("--summary-path", choices=["fused", "separate"], default="fused",
                     help="c5: summary partials in the pileup sweep + one fold (fused), or bc_pileup "
                          "then bc_summary per contig (separate)")
+    ap.add_argument("--tile-index", choices=["on", "off"], default="on",
+                    help="off: drop the upload's per-tile read ranges (bc_reads.tile_reads), A/B only")
     ap.add_argument("--allow-diag", action="store_true",
                     help="run a diagnostic (BC_DIAG) build; its numbers are marked as such")
     args = ap.parse_args()
@@ -601,7 +607,7 @@ def main():
                        "parallelism": f"contig-sharded x{world}",
                        "comm": (group.backend if group is not None else None),
                        "shape": args.shape, "tile_waves": args.tile_waves,
-                       "summary_path": args.summary_path, "build": build},
+                       "summary_path": args.summary_path, "tile_index": args.tile_index, "build": build},
             "gbases_piled_per_s": head["gbases_piled_per_s"],
             "device_us_per_step": head["device_us_per_step"],
             "kernel_us": head["kernel_us"],

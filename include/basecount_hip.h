@@ -42,7 +42,7 @@ extern "C" {
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
 #define BC_E_COMM (-5)  /* RCCL error in a multi-GPU call                                        */
 
-#define BC_ABI_VERSION 3
+#define BC_ABI_VERSION 4
 
 /* Layouts of bc_reads.seq.
  *   BC_SEQ_BAM   BAM packing: "=ACMGRSVTWYHKDBN" codes, two per byte, high nibble first
@@ -82,6 +82,13 @@ typedef struct bc_reads {
     int64_t max_end;          /* upper bound of pos[i] + span[i] over the batch                */
     int32_t seq_layout;       /* BC_SEQ_BAM or BC_SEQ_EVENT                                    */
     int32_t reserved;         /* 0                                                             */
+    /* Optional device index of a sorted batch (NULL / 0: the tiled kernel searches pos[]).  For
+     * the 64-position tile t < n_tiles, tile_reads[2t] and tile_reads[2t+1] are the reads
+     * [lo, hi) that can overlap it: lo = first i with pos[i] > 64t - max_span, hi = first i with
+     * pos[i] >= 64t + 64 (so valid for this max_span only).  bc_reads_upload builds it for dense
+     * batches (fewer tiles than reads/16, fewer than 2^31 reads); host inputs ignore it.       */
+    const int32_t* tile_reads;
+    int64_t n_tiles;
 } bc_reads;
 
 typedef struct bc_ctx bc_ctx;

@@ -265,6 +265,76 @@ def test_fused_pileup_matches_oracle(ctx, seed, L, n, mbq, show_n, path):
     assert np.array_equal(ent, oent) and np.array_equal(sec, osec)  # glibc log2 on the device
 
 
+def _tile_index(ctx, r):
+    n = int(r.r.n_tiles)
+    if n == 0 or not r.r.tile_reads:
+        return None
+    out = np.zeros(2 * n, np.int32)
+    D.check(D.lib().bc_memcpy_d2h(ctx.h, out.ctypes.data, r.r.tile_reads, out.nbytes))
+    ctx.sync()
+    return out.reshape(n, 2)
+
+
+@pytest.mark.parametrize("seed,L,n", [(21, 29_903, 30_000), (22, 700, 5_000), (23, 1_000_000, 2_000)])
+def test_tile_index_matches_searchsorted(ctx, seed, L, n):
+    """bc_reads_upload's tile index (bc_reads.tile_reads) is the range the tiled kernel would
+    search for: [first pos > 64t - max_span, first pos >= 64t + 64) for every tile up to
+    max_end; absent for sparse batches (more tiles than reads / 16)."""
+    rng = np.random.default_rng(seed)
+    b = random_batch(rng, L, n)
+    r = D.DeviceReads(ctx, b)
+    idx = _tile_index(ctx, r)
+    tiles = (int(r.r.max_end) + 63) // 64
+    if tiles > len(b["pos"]) // 16:
+        assert idx is None
+    else:
+        t = np.arange(tiles, dtype=np.int64) * 64
+        pos = b["pos"].astype(np.int64)
+        assert idx.shape == (tiles, 2)
+        assert np.array_equal(idx[:, 0], np.searchsorted(pos, t - int(r.r.max_span) + 1, "left"))
+        assert np.array_equal(idx[:, 1], np.searchsorted(pos, t + 64, "left"))
+    r.free()
+
+
+@pytest.mark.parametrize("L_extra", [0, 5_000, -120])
+def test_pileup_same_without_tile_index(ctx, L_extra):
+    """The tiled kernel gives identical outputs (and the same first out-of-range read) from the
+    tile index and from its own search, including tiles past the index (L > max_end) and edge
+    tiles past L (reads beyond the reference end)."""
+    ctx.set_shape("tile_no_solo")
+    rng = np.random.default_rng(31)
+    L0 = 8_000
+    b = random_batch(rng, L0, 12_000)
+    L = L0 + L_extra
+    outs = []
+    for use in (True, False):
+        r = D.DeviceReads(ctx, b)
+        assert (r.r.n_tiles > 0) and r.r.tile_reads
+        if not use:
+            r.r.tile_reads = None
+            r.r.n_tiles = 0
+        k = 5
+        bufs = [ctx.alloc(max(8, x)) for x in (4 * k * L, 4 * L, 8 * k * L, 8 * L, 8 * L)]
+        nf, nf2 = norm_factors(k)
+        try:
+            ctx.pileup(r, L, 0, k, nf, nf2, *[x.ptr for x in bufs])
+            err = None
+        except D.BcError as e:
+            err = e.code
+        bad = ctx.range_error()
+        outs.append((err, bad, bufs[0].download(np.int32, k * L), bufs[1].download(np.int32, L),
+                     bufs[3].download(np.float64, L)))
+        r.free()
+    (e1, b1, *o1), (e2, b2, *o2) = outs
+    assert e1 == e2 and b1 == b2
+    exp, (br, _) = O.bcount(L, 0, b)
+    assert b1 == br and (br >= 0) == (L_extra < 0)  # reads beyond a shortened reference
+    if br == -1:
+        assert np.array_equal(o1[0].reshape(5, L), exp[:, :5].T.astype(np.int32))
+    for x, y in zip(o1, o2):
+        assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("path", ["tile", "rc"])
 def test_fused_pileup_range_error(ctx, path):
     ctx.set_shape(path)

@@ -22,6 +22,7 @@
 
 #include "bc_internal.h"
 #include "bc_log2.h"
+#include "bc_stats.h"
 
 namespace bc {
 namespace {
@@ -667,47 +668,11 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
 
 // ---- sparse batches (at most ~48 reads per tile): one wave per tile, tiles swept in order ----
 
-// Kernel 2 for one position from its counts (main.py:29-53 in CPython's order, the same
-// arithmetic as tile_terms + the ordered sums of k_pileup), written by the position's lane.
+// Kernel 2 for one position from its counts (bc_stats.h: the same arithmetic as tile_terms + the
+// ordered sums of k_pileup), written by the position's lane.
 template <int K>
 __device__ __forceinline__ double pos_stats(const PileArgs& A, const uint32_t* c, int64_t P) {
-    const int64_t L = A.L;
-    int64_t cov = 0;
-    int am = 0;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        cov += c[j];
-        if (c[j] > c[am]) am = j;  // np.argmax: first maximum
-    }
-    A.cov[P] = (int32_t)cov;
-    double h = 1.0, h2 = 1.0;
-    if (cov != 0) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const double pj = (double)c[j] / (double)cov;
-            if (A.pc) A.pc[(int64_t)j * L + P] = 100.0 * pj;
-            if (c[j] != 0) s = s + (-(pj * glibc_log2(pj)));
-        }
-        h = A.nf * s;
-        const int64_t cov2 = cov - c[am];
-        if (cov2 != 0) {
-            double s2 = 0.0;
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                if (j != am && c[j] != 0) {
-                    const double q = (double)c[j] / (double)cov2;
-                    s2 = s2 + (-(q * glibc_log2(q)));
-                }
-            h2 = A.nf2 * s2;
-        }
-    } else if (A.pc) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) A.pc[(int64_t)j * L + P] = -1.0;
-    }
-    A.ent[P] = h;
-    A.sec[P] = h2;
-    return h;
+    return position_stats<K>(c, A.L, P, A.nf, A.nf2, A.cov, A.pc, A.ent, A.sec);
 }
 
 // numpy's pairwise_sum of one 128-element leaf (pw_leaf of bc_kernels.hip for n = 128) from two

@@ -173,6 +173,48 @@ def test_rc_event_image_shapes(ctx, mix, mbq, ncols):
     assert np.array_equal(got, exp[:, :ncols].T.astype(np.int32)), mix
 
 
+@pytest.mark.parametrize("mix", ["image", "fallback", "mixed"])
+@pytest.mark.parametrize("mbq,k", [(0, 5), (20, 6)])
+def test_rc_pileup_shapes(ctx, mix, mbq, k):
+    """bc_pileup through k_rc + k_stats on image chunks (deferred flush), run-table chunks and
+    complex reads: counts and statistics exact, and repeated calls show the context's
+    accumulation scratch left zeroed."""
+    ctx.set_shape("rc")
+    tpl = {"image": IMAGE_OK, "fallback": FALLBACK, "mixed": IMAGE_OK + FALLBACK[:2]}[mix]
+    rng = np.random.default_rng({"image": 41, "fallback": 42, "mixed": 43}[mix])
+    L = 12_000
+    b = shaped_batch(rng, L, 40_000, tpl)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    ocov, opc, oent, osec = O.stats(exp, k == 6)
+    for rep in range(2):
+        (cnt, cov, pc, ent, sec), bad = gpu_pileup(ctx, b, L, mbq, k)
+        assert bad == -1
+        assert np.array_equal(cnt, exp[:, :k].T.astype(np.int32)), (mix, rep)
+        assert np.array_equal(cov, ocov) and np.array_equal(pc, opc)
+        assert np.array_equal(ent, oent) and np.array_equal(sec, osec)
+
+
+def test_rc_pileup_after_range_error(ctx):
+    """A k_rc bc_pileup call with reads past the reference end: the first offending read, and
+    the next call on the same context is exact (the scratch left zeroed)."""
+    ctx.set_shape("rc")
+    rng = np.random.default_rng(44)
+    L = 5_000
+    b = shaped_batch(rng, L + 400, 30_000, IMAGE_OK[:4])
+    _, (br, _) = O.bcount(L, 0, b)
+    assert br != -1
+    _, bad = gpu_pileup(ctx, b, L, 0, 5)
+    assert bad == br
+    L2 = L + 400
+    exp, (br2, _) = O.bcount(L2, 0, b)
+    assert br2 == -1
+    (cnt, cov, _, ent, _), bad2 = gpu_pileup(ctx, b, L2, 0, 5)
+    assert bad2 == -1 and np.array_equal(cnt, exp[:, :5].T.astype(np.int32))
+    ocov, _, oent, _ = O.stats(exp, False)
+    assert np.array_equal(cov, ocov) and np.array_equal(ent, oent)
+
+
 def test_rc_event_image_range_error(ctx):
     """A read running past the reference end inside an imaged chunk: the reference's first
     offending read (std::out_of_range), nothing counted past L."""

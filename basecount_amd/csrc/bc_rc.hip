@@ -210,6 +210,12 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         fsn_last = A.seq_nib[b0 + n - 1];
     };
     fetch_fields(blockIdx.x);
+    // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
+    // with qualities and six columns, which sit at the VGPR cap without it
+    constexpr bool kPfOn = !(QUAL && NC == 6);
+    constexpr int kPf = 6;
+    uint32_t pw[kPf] = {0u, 0u, 0u, 0u, 0u, 0u};
+    bool pf_ok = false;
 
     // An image chunk's counts (fin, in the image path's otherwise unused hist region) are flushed
     // by wave 3 during the NEXT image chunk's sum, in which it has no rows: waves 0-2 then never
@@ -264,10 +270,15 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         auto decode = [&](auto nslot) {
             if (valid) {
                 uint32_t w[kPre];
+                const bool use_pf = kPfOn && pf_ok && cmax <= kPf;  // (uniform)
 #pragma unroll
                 for (int i = 0; i < kPre; ++i) {
                     w[i] = 0u;
-                    if (i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
+                    if (use_pf && i < kPf) {
+                        w[i] = pw[i];
+                        continue;
+                    }
+                    if (!use_pf && i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
                 }
                 T = decode_runs<decltype(nslot)::value>(w, mcn, cmax);
             }
@@ -373,6 +384,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
         __syncthreads();  // stage, records and the complex-read list complete
         RC_STAMP(3);
+        if (kPfOn) fetch_fields(chunk + gridDim.x);  // back before the CIGAR prefetch below
         if (img_path) {
             // ---- event image: thread tid writes column tid, rows = the chunk's windows
             // [G0, G0 + NWc): the 8 event classes its read has in each (zero outside the read)
@@ -453,7 +465,18 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 expand(std::false_type{}, std::false_type{});
             }
         }
-        fetch_fields(chunk + gridDim.x);  // in flight during the walk
+        pf_ok = false;
+        if (!kPfOn) {
+            fetch_fields(chunk + gridDim.x);  // in flight during the walk
+        } else if (chunk + gridDim.x < A.n_chunks) {
+            const int64_t nb0 = (chunk + gridDim.x) * kRcReads;
+            const int nn = (int)(A.n - nb0 < kRcReads ? A.n - nb0 : kRcReads);
+            const bool nv = tid < nn;
+            const int ncm = (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
+#pragma unroll
+            for (int i = 0; i < kPf; ++i) pw[i] = (nv && i < ncm && (uint32_t)i < fcn) ? A.cigar[fcb + i] : 0u;
+            pf_ok = true;
+        }
         const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
                          staged ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
         const int64_t WB = P0 & ~(int64_t)7;

@@ -694,6 +694,14 @@ __device__ __forceinline__ double leaf_half(double ea, int lane, double* tr) {
     __builtin_amdgcn_wave_barrier();
     return r;
 }
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) of lanes 0-7 (through tr)
+__device__ __forceinline__ double leaf_combine(double r, int lane, double* tr) {
+    if (lane < 8) tr[lane] = r;
+    __builtin_amdgcn_wave_barrier();
+    const double leaf = ((tr[0] + tr[1]) + (tr[2] + tr[3])) + ((tr[4] + tr[5]) + (tr[6] + tr[7]));
+    __builtin_amdgcn_wave_barrier();
+    return leaf;
+}
 __device__ __forceinline__ double leaf_finish(double r, double eb, int lane, double* tr) {
     tr[lane] = eb;
     __builtin_amdgcn_wave_barrier();
@@ -704,11 +712,14 @@ __device__ __forceinline__ double leaf_finish(double r, double eb, int lane, dou
 #pragma unroll
     for (int i = 0; i < 8; ++i) r = r + v[i];
     __builtin_amdgcn_wave_barrier();
-    if (lane < 8) tr[lane] = r;
-    __builtin_amdgcn_wave_barrier();
-    const double leaf = ((tr[0] + tr[1]) + (tr[2] + tr[3])) + ((tr[4] + tr[5]) + (tr[6] + tr[7]));
-    __builtin_amdgcn_wave_barrier();
-    return leaf;
+    return leaf_combine(r, lane, tr);
+}
+// The same for a tile with no reads (every entropy 1.0): no transposition needed.  The half is
+// 1.0 + 1.0 + ... = 8.0 exactly; two such tiles make the leaf 128.0 exactly.
+__device__ __forceinline__ double leaf_finish_ones(double r, int lane, double* tr) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r = r + 1.0;
+    return leaf_combine(r, lane, tr);
 }
 
 __device__ __forceinline__ long long wave_sum_i64(long long v) {
@@ -767,6 +778,7 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     // per quarter) and are added pairwise across the lanes once the quarter is complete; the fold
     // kernel joins the 4 quarters of a buffer
     double e_prev = 0.0;
+    bool prev_empty = false;
     double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + 128 * wave;
     double* mytr = myleaves + 64;  // transposition scratch of the leaf sums
     long long sum_cov = 0, sum_nz = 0;
@@ -812,24 +824,30 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
                 if (lane == 0 && bad != INT64_MAX) atomicMin(A.err, (unsigned long long)bad);
             }
         }
+        const bool empty = hi <= lo;  // (uniform) no read overlaps the tile: all counts zero
         if (t0 < L && P < L && !(BC_ABL(A) & 16)) {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
-                int32_t* dst = A.counts + (int64_t)c * L + P;
-                if (A.accumulate) cnt[c] += (uint32_t)*dst;
-                *dst = (int32_t)cnt[c];
+                int32_t* cb = A.counts + ((int64_t)c * L + t0);  // (uniform)
+                if (A.accumulate) cnt[c] += (uint32_t)cb[lane];
+                cb[lane] = (int32_t)cnt[c];
             }
             if (STATS) {
+                // (an explicit zero-coverage branch here costs registers: the kernel spills)
                 const double h = pos_stats<K>(A, cnt, P);
                 if (SUMP) {
                     static_assert(kNpBuf == 8192 && kNpBuf == 128 * kTile, "buffers of 128 tiles");
                     const int64_t ch = t0 >> 13;  // 8192-position buffer
                     if (ch < A.full_chunks) {
-                        const uint32_t cov = cnt[0] + cnt[1] + cnt[2] + cnt[3] + cnt[4] + (K == 6 ? cnt[5] : 0u);
-                        sum_cov += cov;
-                        sum_nz += cov != 0;
+                        if (!empty) {
+                            const uint32_t cov = cnt[0] + cnt[1] + cnt[2] + cnt[3] + cnt[4] + (K == 6 ? cnt[5] : 0u);
+                            sum_cov += cov;
+                            sum_nz += cov != 0;
+                        }
                         if (t & 1) {
-                            const double lf = leaf_finish(e_prev, h, lane, mytr);
+                            const double lf = (prev_empty && empty) ? 128.0
+                                              : empty                 ? leaf_finish_ones(prev_empty ? 8.0 : e_prev, lane, mytr)
+                                                      : leaf_finish(prev_empty ? 8.0 : e_prev, h, lane, mytr);
                             const int leaf = (int)((t >> 1) & 15);
                             if (lane == 0) myleaves[leaf] = lf;
                             if (leaf == 15) {  // the quarter is complete: its 16 leaves, pairwise
@@ -850,7 +868,8 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
                                 sum_cov = sum_nz = 0;
                             }
                         } else {
-                            e_prev = leaf_half(h, lane, mytr);  // the first tile's half of the chains
+                            prev_empty = empty;  // an empty first tile's half is 8.0 (leaf_finish_ones)
+                            if (!empty) e_prev = leaf_half(h, lane, mytr);  // its half of the chains
                         }
                     }
                 }

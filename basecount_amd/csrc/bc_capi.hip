@@ -219,6 +219,7 @@ int bc_ctx_create(int device, void* stream, bc_ctx** out) {
         c->own_stream = true;
     }
     hipError_t e = hipMalloc(&c->d_err, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sig, hipEventDisableTiming);
     if (e == hipSuccess) e = hipHostMalloc(&c->h_err, sizeof(unsigned long long), hipHostMallocDefault);
     if (e == hipSuccess) e = hipMemsetAsync(c->d_err, 0xFF, sizeof(unsigned long long), c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -244,6 +245,7 @@ int bc_ctx_destroy(bc_ctx* c) {
         }
     for (auto& e : c->mark)
         if (e) (void)hipEventDestroy(e);
+    if (c->sig) (void)hipEventDestroy(c->sig);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return BC_OK;
@@ -590,6 +592,16 @@ int bc_timing_report(bc_ctx* c, int64_t* launches, double* mean_us) {
         mean_us[id] = c->ev[id].empty() ? 0.0 : tot * 1e3 / (double)c->ev[id].size();
         c->ev[id].clear();
     }
+    return BC_OK;
+}
+
+int bc_ctx_wait(bc_ctx* c, bc_ctx* other) {
+    if (!c || !other) return fail(BC_E_ARG, "NULL argument");
+    if (c->device != other->device) return fail(BC_E_ARG, "bc_ctx_wait: contexts on different devices");
+    if (c == other || c->stream == other->stream) return BC_OK;
+    DeviceGuard g(c->device);
+    HIP_TRY(hipEventRecord(other->sig, other->stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, other->sig, 0));
     return BC_OK;
 }
 

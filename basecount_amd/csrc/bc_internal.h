@@ -20,6 +20,7 @@ struct bc_ctx {
     bool timing = false;                  // bc_timing_enable: hipEvents around every launch
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[BC_KERNEL_IDS];
     hipEvent_t mark[BC_EVENT_SLOTS] = {};   // bc_event_record slots (created on first use)
+    hipEvent_t sig = nullptr;               // bc_ctx_wait: "everything enqueued so far"
     int32_t* rc_scratch = nullptr;         // bc_pileup's k_rc accumulation buffer, kept zeroed
     size_t rc_scratch_bytes = 0;
     // kernel-shape overrides (bc_ctx_set_shape); 0 = chosen from the batch

@@ -98,6 +98,7 @@ def lib() -> C.CDLL:
         "bc_timing_enable": ([vp, C.c_int], C.c_int),
         "bc_timing_report": ([vp, vp, vp], C.c_int),
         "bc_event_record": ([vp, C.c_int], C.c_int),
+        "bc_ctx_wait": ([vp, vp], C.c_int),
         "bc_event_elapsed_ms": ([vp, C.c_int, C.c_int, C.POINTER(C.c_float)], C.c_int),
         # multi-GPU (bc_comm.hip)
         "bc_comm_unique_id": ([vp], C.c_int),
@@ -318,6 +319,10 @@ class Context:
         """BAM-packed sequence -> BC_SEQ_EVENT (d_event may alias d_bam; it needs
         seq_event_bytes(seq_bytes) bytes)."""
         check(lib().bc_seq_to_event(self.h, d_bam, int(seq_bytes), d_event))
+
+    def wait(self, other: "Context") -> None:
+        """bc_ctx_wait: this context's later work waits for everything enqueued on `other`."""
+        check(lib().bc_ctx_wait(self.h, other.h))
 
     def event_record(self, slot: int) -> None:
         """Record hipEvent `slot` on the context's stream (region timing)."""

@@ -195,7 +195,7 @@ class Workload:
     """One config's contigs for this rank, resident in HBM before anything is timed."""
 
     def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool,
-                 fused_summary: bool = True, tile_index: bool = True):
+                 fused_summary: bool = True, tile_index: bool = True, streams: int = 1):
         from basecount_amd import device as D
         from basecount_amd import synth
         from basecount_amd.bam import seq_to_event
@@ -244,10 +244,23 @@ class Workload:
             self.work.append((t, L, b, reads, bufs))
         # every contig's 4 summary doubles, contiguous: the rank's gather payload
         self.d_sum = ctx.alloc(32 * max(1, len(self.work))) if summarise else None
+        # contigs are independent: with streams > 1 they run on several contexts' streams at once
+        # (bc_ctx_wait fork / join around them), so one launch's tail overlaps the next launches;
+        # contigs go to the streams longest first, each to the least loaded one (LPT)
+        self.ctxs = [ctx] + [D.Context(ctx.device) for _ in range(max(1, streams) - 1)] if self.per_contig else [ctx]
+        load = [0] * len(self.ctxs)
+        self.on = [0] * len(self.work)
+        for i in sorted(range(len(self.work)), key=lambda i: -self.work[i][1]):
+            j = min(range(len(load)), key=load.__getitem__)
+            self.on[i] = j
+            load[j] += self.work[i][1]
 
     def step(self):
-        ctx = self.ctx
+        main = self.ctx
+        for side in self.ctxs[1:]:  # fork
+            side.wait(main)
         for i, (_, L, _, reads, o) in enumerate(self.work):
+            ctx = self.ctxs[self.on[i]]
             pc = o["pc"].ptr if o["pc"] is not None else None
             if self.summarise and self.fused_summary:  # kernels 1 + 2 and the summary's partials
                 ctx.pileup_partials(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr,
@@ -259,6 +272,9 @@ class Workload:
             else:
                 ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
                            pc, o["ent"].ptr, o["sec"].ptr)
+        for side in self.ctxs[1:]:  # join
+            main.wait(side)
+        ctx = main
         if self.summarise and self.fused_summary:  # every contig's fold, side by side
             ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
                              [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
@@ -346,7 +362,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     from basecount_amd import device as D
 
     wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused",
-                  args.tile_index == "on")
+                  args.tile_index == "on", args.streams if summarise else 1)
     rccl = group is not None and getattr(group, "backend", "") == "rccl"
     gather = None
     if summarise and group is not None:
@@ -414,15 +430,18 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         # sweep (with its partial sums) and the summary's tail + fold, per step
         reps_t = max(2, min(steps, 5))
         ctx.sync()
-        ctx.timing(True)
+        for c in wl.ctxs:
+            c.timing(True)
         for _ in range(reps_t):
             wl.step()
-        rep = ctx.timing_report()
-        ctx.timing(False)
+        rep = {}
+        for c in wl.ctxs:  # every context's launches (several streams: durations overlap)
+            for name, (n_launch, mean_us) in c.timing_report().items():
+                rep[name] = rep.get(name, 0.0) + n_launch * mean_us
+            c.timing(False)
         for name in ("pileup", "rc", "stats", "summary"):
             if name in rep:
-                n_launch, mean_us = rep[name]
-                kern_s[name] = n_launch * mean_us * 1e-6 / reps_t
+                kern_s[name] = rep[name] * 1e-6 / reps_t
     elif "pileup" in launched:
         def pile_only():
             for _, L, _, reads, o in wl.work:
@@ -456,7 +475,10 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         parity = all(v[0] == 1 for v in group.all_gather_ints([int(parity)]))
 
     kbytes = wl.bytes_dominant(dom)
-    achieved = kbytes / kern_s[dom] / 1e9
+    # with several streams the launches overlap, so their summed durations exceed the step: the
+    # roofline then uses the whole step's device time (fold included), a lower bound
+    basis_s = dev_step if len(wl.ctxs) > 1 else kern_s[dom]
+    achieved = kbytes / basis_s / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "kernel1_pmc.json")
     if os.path.exists(pmc) and world == 1:
@@ -485,9 +507,12 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         "reads_per_rank": int(sum(int(w[2]["pos"].size) for w in wl.work)),
         "positions_per_rank": int(sum(w[1] for w in wl.work)),
         "contigs_per_rank": len(wl.work),
+        "streams": len(wl.ctxs),
         "parity_vs_oracle": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_NAMES[dom],
+                     "time_basis": ("device time per step, %d streams" % len(wl.ctxs)) if len(wl.ctxs) > 1
+                     else "kernel's average duration",
                      "algorithmic_bytes": kbytes},
     }
     if gather_us is not None:
@@ -516,6 +541,8 @@ def main():
     ap.add_argument("--summary-path", choices=["fused", "separate"], default="fused",
                     help="c5: summary partials in the pileup sweep + one fold (fused), or bc_pileup "
                          "then bc_summary per contig (separate)")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="c5: contexts (streams) the contigs run on concurrently (bc_ctx_wait fork/join)")
     ap.add_argument("--tile-index", choices=["on", "off"], default="on",
                     help="off: drop the upload's per-tile read ranges (bc_reads.tile_reads), A/B only")
     ap.add_argument("--allow-diag", action="store_true",

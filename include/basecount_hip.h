@@ -184,6 +184,12 @@ int bc_graph_end(bc_ctx* ctx, bc_graph** out);
 int bc_graph_launch(bc_ctx* ctx, bc_graph* g);
 int bc_graph_destroy(bc_graph* g);
 
+/* Stream order between two contexts of one device: ctx's later work waits for everything enqueued
+ * on other's stream so far (an event, no host wait).  Independent references can then run on
+ * several contexts' streams at once, e.g. inside a capture begun on `main`: fork with
+ * bc_ctx_wait(side, main), enqueue on each, join with bc_ctx_wait(main, side).                */
+int bc_ctx_wait(bc_ctx* ctx, bc_ctx* other);
+
 /* Per-kernel timing (SURVEY §5 tracing): when enabled, every launch made through the context is
  * bracketed by hipEvents on its stream.  bc_timing_report() synchronises and returns, per kernel
  * id (BC_K_*), the number of timed launches and their mean duration in microseconds, then clears

@@ -646,6 +646,57 @@ def test_summary_fold_many_references(ctx):
         assert np.array_equal(dout.download(np.float64, 4), e)
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_ctx_wait_fork_join(ctx, graph):
+    """References spread over three contexts' streams, forked from and joined back into the main
+    context with bc_ctx_wait (eagerly, and captured into one graph begun on the main context):
+    every reference's outputs and the main context's fold equal single-stream results."""
+    rng = np.random.default_rng(78)
+    k = 5
+    nf, nf2 = norm_factors(k)
+    sides = [D.Context(ctx.device), D.Context(ctx.device)]
+    ctxs = [ctx] + sides
+    refs = []
+    for i in range(9):
+        L = int(rng.choice([8192 * 3 + 11, 40_000, 150_000]))
+        b = random_batch(rng, L, int(rng.integers(200, 4000)))
+        r = D.DeviceReads(ctx, b)
+        bufs = [ctx.alloc(max(8, x)) for x in (4 * k * L, 4 * L, 8 * L, 8 * L)]
+        work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        exp, _ = O.bcount(L, 0, b)
+        refs.append((L, r, bufs, work, dout, exp))
+
+    def step():
+        for s in sides:
+            s.wait(ctx)
+        for i, (L, r, bufs, work, dout, _) in enumerate(refs):
+            ctxs[i % 3].pileup_partials(r, L, 0, k, nf, nf2, bufs[0].ptr, bufs[1].ptr, None, bufs[2].ptr,
+                                        bufs[3].ptr, work.ptr)
+        for s in sides:
+            ctx.wait(s)
+        ctx.summary_fold([x[0] for x in refs], [x[3].ptr for x in refs], [x[4].ptr for x in refs])
+
+    if graph:
+        g = ctx.capture(step)
+        g.launch()
+        g.launch()  # a replay over the same buffers gives the same results
+    else:
+        step()
+    ctx.sync()
+    for c in ctxs:
+        assert c.range_error() == -1
+    for L, r, bufs, work, dout, exp in refs:
+        cnt = bufs[0].download(np.int32, k * L).reshape(k, L)
+        cov = bufs[1].download(np.int32, L)
+        ent = bufs[2].download(np.float64, L)
+        assert np.array_equal(cnt, exp[:, :k].T.astype(np.int32))
+        ocov, _, oent, _ = O.stats(exp, False)
+        assert np.array_equal(cov, ocov) and np.array_equal(ent, oent)
+        w2, d2 = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        ctx.summary(bufs[1].ptr, bufs[2].ptr, L, w2.ptr, d2.ptr)
+        assert np.array_equal(dout.download(np.float64, 4), d2.download(np.float64, 4))
+
+
 def test_cli_timing_report_keeps_stdout(golden, manifest, tmp_path):
     """BASECOUNT_HIP_TIMING=1: kernel times and the wall time on stderr, stdout still
     byte-identical to the reference's."""

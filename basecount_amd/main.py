@@ -180,6 +180,34 @@ def _alloc_outputs(ctx, k, L, want_pc):
     return o
 
 
+class _Scratch:
+    """Device buffers reused from reference to reference within one get_basecounts call, grown
+    (never shrunk) on demand: at GRCh38 sizes the per-reference outputs are GB-sized, and a
+    hipMalloc / hipFree (which synchronises) per reference and buffer cost more than the
+    kernels.  Every use is stream-ordered after the previous reference's kernels, and rows are
+    downloaded before the next reference starts."""
+
+    def __init__(self, ctx):
+        self.ctx, self.bufs = ctx, {}
+
+    def get(self, role: str, nbytes: int):
+        b = self.bufs.get(role)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                b.free()
+            b = self.bufs[role] = self.ctx.alloc(max(16, int(nbytes)))
+        return b
+
+    def outputs(self, k, L, want_pc):
+        return {"cov": self.get("cov", 4 * L), "ent": self.get("ent", 8 * L), "sec": self.get("sec", 8 * L),
+                "pc": self.get("pc", 8 * k * L) if want_pc else None}
+
+    def release(self):
+        for b in self.bufs.values():
+            b.free()
+        self.bufs.clear()
+
+
 def _download(outs, counts, k, L) -> RefData:
     cov = outs["cov"].download(np.int32, L)
     ent = outs["ent"].download(np.float64, L)
@@ -414,12 +442,23 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
             ctx = context(device)
             fod = _FileOnDevice(ctx, samfile, sel, need_qual=mbq > 0)
             nf, nf2 = norm_factors(k)
-            for ref in mine:
-                t = ref_index[ref]
-                L = int(reference_lengths[ref])
-                results[ref], range_idx[ref] = _device_reference(
-                    ctx, fod.reads(t), L, mbq, ncols, k, nf, nf2, _mode,
-                    _tiles(ref) if _tiles else None, _tiles is not None)
+            scratch = _Scratch(ctx)
+            try:
+                # sized once for the longest reference
+                Lmax = max(int(reference_lengths[r]) for r in mine)
+                scratch.outputs(k, Lmax, _mode == "rows")
+                scratch.get("hist", 4 * ncols * Lmax)
+                if _mode != "rows":
+                    scratch.get("work", D.summary_work_bytes(Lmax))
+                for ref in mine:
+                    t = ref_index[ref]
+                    L = int(reference_lengths[ref])
+                    results[ref], range_idx[ref] = _device_reference(
+                        ctx, fod.reads(t), L, mbq, ncols, k, nf, nf2, _mode,
+                        _tiles(ref) if _tiles else None, _tiles is not None, scratch)
+            finally:
+                ctx.sync()
+                scratch.release()
         if _group is not None and 0 <= mbq < _U32:
             # every rank needs every reference's first out-of-range read to raise the same error
             alls = _group.all_gather_ints([range_idx.get(r, -2) for r in ref_order])
@@ -444,7 +483,7 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
         samfile.close()
 
 
-def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_tiles=False):
+def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_tiles=False, scratch=None):
     """Kernel 1 + kernel 2 (+ reductions) for one reference; returns (result, first bad read).
 
     Coordinate-sorted batches take the fused tiled kernel (bc_pileup); others count with the
@@ -458,13 +497,14 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
         empty = RefData(np.zeros((k, 0), np.int32), np.zeros((k, 0)), np.zeros(0), np.zeros(0),
                         np.zeros(0, np.int32))
         return (empty if mode == "rows" else {"L": 0}), bad
-    outs = _alloc_outputs(ctx, k, L, want_pc=(mode == "rows"))
-    hist = ctx.alloc(4 * ncols * L)
+    scratch = scratch or _Scratch(ctx)
+    outs = scratch.outputs(k, L, want_pc=(mode == "rows"))
+    hist = scratch.get("hist", 4 * ncols * L)
     pc_ptr = outs["pc"].ptr if outs["pc"] else None
     work = dout = None
     if mode != "rows":
-        work = ctx.alloc(D.summary_work_bytes(L))
-        dout = ctx.alloc(32)
+        work = scratch.get("work", D.summary_work_bytes(L))
+        dout = scratch.get("dout", 32)
     if reads.sorted and mode != "rows":
         # pileup + summary: the sparse sweep computes numpy's buffer partials in registers
         ctx.pileup_summary(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr,
@@ -473,7 +513,7 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
         ctx.pileup(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
                    outs["sec"].ptr)
     else:
-        hist.zero()
+        hist.zero(4 * ncols * L)
         ctx.count(reads, L, mbq, ncols, hist.ptr)
         ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
                   outs["sec"].ptr)

@@ -42,3 +42,15 @@ def test_hip_library_contains_gfx950_code_object():
     with open(os.path.join(REPO, "basecount_amd", "libbasecount_hip.so"), "rb") as fh:
         blob = fh.read()
     assert b"gfx950" in blob
+
+
+def test_hip_library_rejects_null_arguments_without_touching_a_device():
+    """Argument checks come first: NULL contexts / outputs are BC_E_ARG with a message."""
+    from basecount_amd import device as D
+
+    L = D.lib()
+    assert L.bc_ctx_wait(None, None) == D.BC_E_ARG
+    assert b"NULL" in L.bc_last_error()
+    assert L.bc_sync(None) == D.BC_E_ARG
+    assert L.bc_ctx_set_shape(None, 0, 0, 0) == D.BC_E_ARG
+    assert L.bc_pileup(None, None, 0, 0, 5, 0.0, 0.0, None, None, None, None, None) == D.BC_E_ARG

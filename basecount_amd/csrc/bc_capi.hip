@@ -6,9 +6,16 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bc_internal.h"
+
+namespace bc {
+namespace {
+#include "bc_runs.h"
+}  // namespace
+}  // namespace bc
 
 namespace {
 
@@ -109,6 +116,34 @@ std::vector<int32_t> tile_index(const bc_reads& h, int sorted, int max_span, int
         out[2 * t] = (int32_t)lo;
         out[2 * t + 1] = (int32_t)hi;
     }
+    return out;
+}
+
+// bc_reads.read_runs for a sorted batch: every read's CIGAR decoded once (bc::decode_runs, the
+// kernels' own decode) into its 16-byte run record, on up to 16 host threads.
+std::vector<uint32_t> read_runs(const bc_reads& h, int sorted) {
+    std::vector<uint32_t> out;
+    const int64_t n = h.n_reads;
+    if (!sorted || n <= 0) return out;
+    out.resize((size_t)n * 4);
+    auto work = [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            const uint32_t cn = h.cig_n[i];
+            const int c = (int)(cn < (uint32_t)bc::kPre ? cn : (uint32_t)bc::kPre);
+            uint32_t w[bc::kPre] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < c; ++k) w[k] = h.cigar[h.cig_beg[i] + k];
+            bc::pack_runs(bc::decode_runs<2>(w, cn, c), &out[(size_t)i * 4]);
+        }
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int64_t nt = std::min<int64_t>({(int64_t)(hw ? hw : 1), 16, (n + 65535) / 65536});
+    if (nt <= 1) {
+        work(0, n);
+        return out;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+    for (auto& x : th) x.join();
     return out;
 }
 
@@ -342,14 +377,17 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     // the tile index of a dense sorted batch (bc_reads.tile_reads): the read range of every
     // 64-position tile, so the tiled kernel starts each tile with one load instead of a search
     std::vector<int32_t> tidx = tile_index(*h, d->sorted, d->max_span, d->max_end);
-    constexpr int kArr = 8;
-    void* p[kArr] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // the run records of a sorted batch (bc_reads.read_runs): its CIGARs decoded once, here
+    std::vector<uint32_t> runs = read_runs(*h, d->sorted);
+    constexpr int kArr = 9;
+    void* p[kArr] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // the sequence buffer is sized for BC_SEQ_EVENT (converted in place after the copy)
     const size_t sz[kArr] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4,
                              bc::seq_event_bytes(h->seq_bytes), h->qual ? (size_t)h->qual_bytes : 0,
-                             tidx.size() * 4};
-    const size_t cp[kArr] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6], sz[7]};
-    const void* src[kArr] = {h->pos, h->cig_beg, h->cig_n, h->seq_nib, h->cigar, h->seq, h->qual, tidx.data()};
+                             tidx.size() * 4, runs.size() * 4};
+    const size_t cp[kArr] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6], sz[7], sz[8]};
+    const void* src[kArr] = {h->pos,  h->cig_beg, h->cig_n,   h->seq_nib,  h->cigar,
+                             h->seq,  h->qual,    tidx.data(), runs.data()};
     // ONE slab for the whole batch (arrays 4 KiB-aligned inside it, the slab a multiple of 2 MiB):
     // the kernels' first touches of a batch then miss the GPU TLB on a few large fragments
     // instead of on every small buffer's pages.  The first array present is the slab base
@@ -387,8 +425,9 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     d->qual = (const uint8_t*)p[6];
     d->tile_reads = (const int32_t*)p[7];
     d->n_tiles = (int64_t)tidx.size() / 2;
+    d->read_runs = (const uint32_t*)p[8];
     d->seq_layout = BC_SEQ_EVENT;
-    HIP_TRY(hipStreamSynchronize(c->stream));  // also keeps tidx alive until its copy is done
+    HIP_TRY(hipStreamSynchronize(c->stream));  // also keeps tidx / runs alive until their copies are done
     return BC_OK;
 }
 
@@ -396,7 +435,7 @@ int bc_reads_free(bc_ctx* c, bc_reads* d) {
     if (!c || !d) return fail(BC_E_ARG, "NULL argument");
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
-    const void* p[8] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual, d->tile_reads};
+    const void* p[9] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual, d->tile_reads, d->read_runs};
     for (auto q : p)  // the first array present is the base of the batch's slab (bc_reads_upload)
         if (q) {
             (void)hipFree((void*)q);

@@ -86,10 +86,11 @@ struct RcArgs {
     int64_t seq_words;
     int64_t qual_bytes;
     int64_t n_chunks;
+    const uint4* runs;  // bc_reads.read_runs (run records, bc_runs.h) or NULL: decode the CIGARs
     int32_t* counts;  // [ncols][L], accumulated into
     unsigned long long* err;
     int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events,
-                 // 512 no staging, 2048 no flush, 8192 no event image
+                 // 512 no staging, 2048 no flush, 8192 no event image, 16384 no image expansion
     unsigned long long* trace;  // diagnostic only (BC_PHASE_TRACE builds): [block][wave][kRcPhases]
 };
 
@@ -213,6 +214,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
     // with qualities and six columns, which sit at the VGPR cap without it
     constexpr bool kPfOn = !(QUAL && NC == 6);
+    // run records (bc_reads.read_runs) in place of the first decode: the variants with spare
+    // registers (the others spill with the extra path)
+    constexpr bool kRunsOn = !QUAL && NC == 5;
+    const uint4* const runs = kRunsOn ? A.runs : nullptr;
     constexpr int kPf = 6;
     uint32_t pw[kPf] = {0u, 0u, 0u, 0u, 0u, 0u};
     bool pf_ok = false;
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         auto decode = [&](auto nslot) {
             if (valid) {
                 uint32_t w[kPre];
-                const bool use_pf = kPfOn && pf_ok && cmax <= kPf;  // (uniform)
+                const bool use_pf = kPfOn && pf_ok && !runs && cmax <= kPf;  // (uniform)
 #pragma unroll
                 for (int i = 0; i < kPre; ++i) {
                     w[i] = 0u;
@@ -283,7 +288,25 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 T = decode_runs<decltype(nslot)::value>(w, mcn, cmax);
             }
         };
-        decode(std::integral_constant<int, 2>{});
+        if (runs) {  // (uniform) the upload's run records: no CIGAR load, no decode
+            if (valid) {
+                uint4 q;
+                if (kPfOn && pf_ok) q = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+                else q = runs[c0 + tid];
+                T = unpack_runs(q.x, q.y, q.z, q.w);
+            }
+        } else if (BC_ABL(A) & 32768) {  // diagnostic: no CIGAR load / decode (every read one 120-base run)
+            if (valid) {
+                T.nrun = 1;
+                T.st[0] = 0;
+                T.en[0] = 120;
+                T.qd[0] = 0;
+                T.span = 120;
+                T.qlen = 120;
+            }
+        } else {
+            decode(std::integral_constant<int, 2>{});
+        }
         const bool cx = valid && T.complex;
         const bool simple = valid && !cx;
         if (tid == 0) ncx = 0;
@@ -454,7 +477,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     img[tid * kImgRows + row] = x;
                 }
             };
-            if (!simple) {
+            if (!simple || (BC_ABL(A) & 16384)) {
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) img[tid * kImgRows + row] = 0u;
             } else if (8 * (int64_t)(G0 + kImgRows) > A.L) {  // (uniform) rows may reach past L
@@ -472,9 +495,16 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const int64_t nb0 = (chunk + gridDim.x) * kRcReads;
             const int nn = (int)(A.n - nb0 < kRcReads ? A.n - nb0 : kRcReads);
             const bool nv = tid < nn;
-            const int ncm = (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
+            if (runs) {  // (uniform) the next chunk's run records instead of its CIGAR words
+                if (nv) {
+                    const uint4 q = runs[nb0 + tid];
+                    pw[0] = q.x, pw[1] = q.y, pw[2] = q.z, pw[3] = q.w;
+                }
+            } else {
+                const int ncm = (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
 #pragma unroll
-            for (int i = 0; i < kPf; ++i) pw[i] = (nv && i < ncm && (uint32_t)i < fcn) ? A.cigar[fcb + i] : 0u;
+                for (int i = 0; i < kPf; ++i) pw[i] = (nv && i < ncm && (uint32_t)i < fcn) ? A.cigar[fcb + i] : 0u;
+            }
             pf_ok = true;
         }
         const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
@@ -734,6 +764,7 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     A.mbq = mbq;
     A.seq_words = (int64_t)(seq_event_bytes(r.seq_bytes) / 4);
     A.qual_bytes = r.qual ? r.qual_bytes : 0;
+    A.runs = r.read_runs && !((uintptr_t)r.read_runs & 15u) ? (const uint4*)r.read_runs : nullptr;
     A.counts = counts;
     A.err = d_err;
     A.ablate = 0;

@@ -1,0 +1,115 @@
+// bc_runs.h — a read's CIGAR as a run table (count.cpp:40-96 semantics), on the device and on the
+// host.  The kernels decode CIGAR words into these tables; bc_reads_upload decodes each read of a
+// sorted batch once, with the same function, into a 16-byte run record (bc_reads.read_runs) that
+// the read-chunked kernel then loads instead of decoding.
+//
+// Included inside namespace bc::{anonymous} of each kernel file (through bc_walk.h) and of
+// bc_capi.hip.
+#pragma once
+#include <cstdint>
+
+#ifndef BC_HD
+#define BC_HD __host__ __device__ __forceinline__
+#endif
+
+constexpr int kPre = 8;  // CIGAR words decoded per read (more -> complex path)
+
+BC_HD bool mlike(uint32_t op) { return op == 0 || op == 7 || op == 8; }
+BC_HD bool dlike(uint32_t op) { return op == 2 || op == 3; }
+BC_HD bool qcons(uint32_t op) { return op == 0 || op == 1 || op == 7 || op == 8; }
+
+// Run table of a read: its aligned (M/=/X) bases as at most 4 runs [st, en) of reference
+// offsets from the read start, each with a query delta qd (query offset = reference offset +
+// qd; consecutive M/=/X ops with the same delta merge, so the M/=/X distinction and S/H/P
+// between them vanish).  Every other reference offset in [0, span) is a deletion / ref-skip.
+// count.cpp:40-96 semantics: M/=/X consume both, I the query only, D/N the reference only.
+constexpr int kMaxRuns = 4;
+
+struct RunTable {
+    uint32_t st[kMaxRuns], en[kMaxRuns];
+    int32_t qd[kMaxRuns];
+    uint32_t span;
+    uint32_t qlen;  // query bases consumed (M/=/X/I) by the decoded ops
+    int nrun;
+    bool gap;       // some reference offset in [0, span) is a deletion / ref-skip
+    bool complex;
+};
+
+// NSLOT < kMaxRuns fills only the first NSLOT runs' st / en / qd (nrun, complex and the rest are
+// those of the full table): callers re-decode with the full table when a read has more runs.
+template <int NSLOT = kMaxRuns>
+BC_HD RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn, int cmax) {
+    // Branch-free: every op updates the table through selects (a divergent if/else chain here
+    // compiles to hundreds of register moves per read).
+    RunTable T;
+#pragma unroll
+    for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
+    bool cx = cn > (uint32_t)kPre, gap = false;
+    uint32_t rc = 0, qc = 0, last_en = 0xFFFFFFFFu;
+    int last_qd = 0, nrun = 0;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+        if (k >= cmax) break;  // wave-uniform: no lane has more ops
+        const uint32_t op = w[k] & 15u, len = (uint32_t)k < cn ? w[k] >> 4 : 0u;
+        const bool m = mlike(op) && len != 0u;  // M/=/X: a run (new, or extending the last one)
+        const bool d = dlike(op) && len != 0u;  // D/N: reference only
+        const int qd = (int)qc - (int)rc;
+        const bool ext = m && last_en == rc && last_qd == qd;
+        const bool nw = m && !ext;
+        cx = cx || (m && (qd < -32768 || qd > 32767)) || (nw && nrun >= kMaxRuns);
+        const uint32_t e = rc + len;
+#pragma unroll
+        for (int i = 0; i < NSLOT; ++i) {
+            const bool sn = nw && nrun == i, se = ext && nrun == i + 1;
+            T.st[i] = sn ? rc : T.st[i];
+            T.qd[i] = sn ? qd : T.qd[i];
+            T.en[i] = (sn || se) ? e : T.en[i];
+        }
+        nrun += nw ? 1 : 0;
+        gap = gap || d;
+        rc = (m || d) ? e : rc;
+        qc += (m || op == 1u) ? len : 0u;  // I: query only
+        last_en = m ? e : last_en;
+        last_qd = m ? qd : last_qd;
+    }
+    T.nrun = nrun;
+    T.gap = gap;
+    T.complex = cx || rc >= 0x1FFFu;
+    T.span = rc;
+    T.qlen = qc;
+    return T;
+}
+
+// The 16-byte run record (bc_reads.read_runs, 4 words per read) of a read's first two runs:
+//   x = st0 | en0 << 13 | min(nrun, 7) << 26 | gap << 29 | complex << 30
+//   y = st1 | en1 << 13
+//   z = qd0 (int16) | qd1 (int16) << 16
+//   w = span | qlen << 16
+// Offsets fit 13 bits and qd 16 (decode_runs marks a read complex otherwise); a read whose query
+// length exceeds 16 bits is recorded as complex.  unpack(pack(T)) equals decode_runs<2>'s table
+// (runs 2 and 3 left empty: a chunk with more runs decodes its CIGARs again).
+BC_HD void pack_runs(const RunTable& T, uint32_t* r) {
+    const bool cx = T.complex || T.qlen > 0xFFFFu;
+    const uint32_t nr = (uint32_t)(T.nrun < 7 ? T.nrun : 7);
+    r[0] = (T.st[0] & 0x1FFFu) | (T.en[0] & 0x1FFFu) << 13 | nr << 26 | (T.gap ? 1u : 0u) << 29 | (cx ? 1u : 0u) << 30;
+    r[1] = (T.st[1] & 0x1FFFu) | (T.en[1] & 0x1FFFu) << 13;
+    r[2] = ((uint32_t)T.qd[0] & 0xFFFFu) | ((uint32_t)T.qd[1] & 0xFFFFu) << 16;
+    r[3] = (T.span & 0xFFFFu) | (T.qlen & 0xFFFFu) << 16;
+}
+BC_HD RunTable unpack_runs(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    RunTable T;
+    T.st[0] = x & 0x1FFFu;
+    T.en[0] = (x >> 13) & 0x1FFFu;
+    T.st[1] = y & 0x1FFFu;
+    T.en[1] = (y >> 13) & 0x1FFFu;
+    T.st[2] = T.en[2] = T.st[3] = T.en[3] = 0;
+    T.qd[0] = (int32_t)(int16_t)(z & 0xFFFFu);
+    T.qd[1] = (int32_t)(int16_t)(z >> 16);
+    T.qd[2] = T.qd[3] = 0;
+    T.nrun = (int)((x >> 26) & 7u);
+    T.gap = ((x >> 29) & 1u) != 0;
+    T.complex = ((x >> 30) & 1u) != 0;
+    T.span = w & 0xFFFFu;
+    T.qlen = w >> 16;
+    return T;
+}

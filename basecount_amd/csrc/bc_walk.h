@@ -9,80 +9,16 @@
 // D/N count DS, I/S/H/P/B count nothing.
 #pragma once
 
+#include "bc_runs.h"
+
 constexpr unsigned long long kNibCol6 = 0x6666666366625106ull;  // class -> column, 6 = none
 constexpr uint32_t kM1 = 0x11111111u;      // bit 0 of every nibble
 constexpr uint32_t kClsDel = 0xCCCCCCCCu;  // class 1100 (deletion / ref-skip) in every nibble
-constexpr int kPre = 8;  // CIGAR words decoded per read (more -> complex path)
 constexpr uint32_t kNone = 0xFFFFFFFFu;  // packed event: none
 constexpr uint32_t kDel = 0x80000000u;   // packed event: deletion / ref-skip
 
 __device__ __forceinline__ unsigned nib_col6(unsigned nib) { return (unsigned)(kNibCol6 >> (nib * 4)) & 0xFu; }
-__device__ __forceinline__ bool mlike(uint32_t op) { return op == 0 || op == 7 || op == 8; }
-__device__ __forceinline__ bool dlike(uint32_t op) { return op == 2 || op == 3; }
-__device__ __forceinline__ bool qcons(uint32_t op) { return op == 0 || op == 1 || op == 7 || op == 8; }
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-
-// Run table of a read: its aligned (M/=/X) bases as at most 4 runs [st, en) of reference
-// offsets from the read start, each with a query delta qd (query offset = reference offset +
-// qd; consecutive M/=/X ops with the same delta merge, so the M/=/X distinction and S/H/P
-// between them vanish).  Every other reference offset in [0, span) is a deletion / ref-skip.
-// count.cpp:40-96 semantics: M/=/X consume both, I the query only, D/N the reference only.
-constexpr int kMaxRuns = 4;
-
-struct RunTable {
-    uint32_t st[kMaxRuns], en[kMaxRuns];
-    int32_t qd[kMaxRuns];
-    uint32_t span;
-    uint32_t qlen;  // query bases consumed (M/=/X/I) by the decoded ops
-    int nrun;
-    bool gap;       // some reference offset in [0, span) is a deletion / ref-skip
-    bool complex;
-};
-
-// NSLOT < kMaxRuns fills only the first NSLOT runs' st / en / qd (nrun, complex and the rest are
-// those of the full table): callers re-decode with the full table when a read has more runs.
-template <int NSLOT = kMaxRuns>
-__device__ __forceinline__ RunTable decode_runs(const uint32_t (&w)[kPre], uint32_t cn, int cmax) {
-    // Branch-free: every op updates the table through selects (a divergent if/else chain here
-    // compiles to hundreds of register moves per read).
-    RunTable T;
-#pragma unroll
-    for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
-    bool cx = cn > (uint32_t)kPre, gap = false;
-    uint32_t rc = 0, qc = 0, last_en = 0xFFFFFFFFu;
-    int last_qd = 0, nrun = 0;
-#pragma unroll
-    for (int k = 0; k < kPre; ++k) {
-        if (k >= cmax) break;  // wave-uniform: no lane has more ops
-        const uint32_t op = w[k] & 15u, len = (uint32_t)k < cn ? w[k] >> 4 : 0u;
-        const bool m = mlike(op) && len != 0u;  // M/=/X: a run (new, or extending the last one)
-        const bool d = dlike(op) && len != 0u;  // D/N: reference only
-        const int qd = (int)qc - (int)rc;
-        const bool ext = m && last_en == rc && last_qd == qd;
-        const bool nw = m && !ext;
-        cx = cx || (m && (qd < -32768 || qd > 32767)) || (nw && nrun >= kMaxRuns);
-        const uint32_t e = rc + len;
-#pragma unroll
-        for (int i = 0; i < NSLOT; ++i) {
-            const bool sn = nw && nrun == i, se = ext && nrun == i + 1;
-            T.st[i] = sn ? rc : T.st[i];
-            T.qd[i] = sn ? qd : T.qd[i];
-            T.en[i] = (sn || se) ? e : T.en[i];
-        }
-        nrun += nw ? 1 : 0;
-        gap = gap || d;
-        rc = (m || d) ? e : rc;
-        qc += (m || op == 1u) ? len : 0u;  // I: query only
-        last_en = m ? e : last_en;
-        last_qd = m ? qd : last_qd;
-    }
-    T.nrun = nrun;
-    T.gap = gap;
-    T.complex = cx || rc >= 0x1FFFu;
-    T.span = rc;
-    T.qlen = qc;
-    return T;
-}
 
 // Wave-wide max / min (result in every lane's SGPR): DPP row prefix, row broadcasts, readlane.
 template <bool MAX>

@@ -42,6 +42,7 @@ class BcReads(C.Structure):
         ("reserved", C.c_int32),
         ("tile_reads", C.c_void_p),  # optional per-tile read ranges (bc_reads_upload)
         ("n_tiles", C.c_int64),
+        ("read_runs", C.c_void_p),  # optional run records, 4 words per read (bc_reads_upload)
     ]
 
 

@@ -195,7 +195,8 @@ class Workload:
     """One config's contigs for this rank, resident in HBM before anything is timed."""
 
     def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool,
-                 fused_summary: bool = True, tile_index: bool = True, streams: int = 1):
+                 fused_summary: bool = True, tile_index: bool = True, streams: int = 1,
+                 read_runs: bool = True):
         from basecount_amd import device as D
         from basecount_amd import synth
         from basecount_amd.bam import seq_to_event
@@ -223,6 +224,9 @@ class Workload:
         self.fused_summary = fused_summary
         self.nf, self.nf2 = norm_factors(self.k)
         self.work = []
+        # host side of bc_reads_upload (its run records and tile index, built once per batch)
+        # + the copies, untimed: reported as upload_ms
+        self.upload_s = 0.0
         ev = None
         for t, L in enumerate(self.rs.lengths):
             b = synth.batch_arrays(self.rs, t, 0)
@@ -230,11 +234,15 @@ class Workload:
                 ev = seq_to_event(b["seq"])
             if mbq == 0:  # qualities are never read without a threshold: not uploaded
                 b = dict(b, qual=None)
+            t_up = time.perf_counter()
             reads = D.DeviceReads(ctx, dict(b, seq_event=ev))
+            self.upload_s += time.perf_counter() - t_up
             assert reads.r.sorted == 1
             if not tile_index:  # A/B: the tiled kernel searches pos[] (the index stays allocated)
                 reads.r.tile_reads = None
                 reads.r.n_tiles = 0
+            if not read_runs:  # A/B: the read-chunked kernel decodes the CIGARs itself
+                reads.r.read_runs = None
             k = self.k
             bufs = dict(counts=ctx.alloc(4 * k * L), cov=ctx.alloc(4 * L),
                         pc=ctx.alloc(8 * k * L) if self.want_pc else None, ent=ctx.alloc(8 * L),
@@ -362,7 +370,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     from basecount_amd import device as D
 
     wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused",
-                  args.tile_index == "on", args.streams if summarise else 1)
+                  args.tile_index == "on", args.streams if summarise else 1, args.read_runs == "on")
     rccl = group is not None and getattr(group, "backend", "") == "rccl"
     gather = None
     if summarise and group is not None:
@@ -508,6 +516,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         "positions_per_rank": int(sum(w[1] for w in wl.work)),
         "contigs_per_rank": len(wl.work),
         "streams": len(wl.ctxs),
+        "upload_ms": wl.upload_s * 1e3,
         "parity_vs_oracle": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_NAMES[dom],
@@ -543,6 +552,8 @@ def main():
                          "then bc_summary per contig (separate)")
     ap.add_argument("--streams", type=int, default=4,
                     help="c5: contexts (streams) the contigs run on concurrently (bc_ctx_wait fork/join)")
+    ap.add_argument("--read-runs", choices=["on", "off"], default="on",
+                    help="off: drop the upload's run records (bc_reads.read_runs), A/B only")
     ap.add_argument("--tile-index", choices=["on", "off"], default="on",
                     help="off: drop the upload's per-tile read ranges (bc_reads.tile_reads), A/B only")
     ap.add_argument("--allow-diag", action="store_true",
@@ -634,9 +645,11 @@ def main():
                        "parallelism": f"contig-sharded x{world}",
                        "comm": (group.backend if group is not None else None),
                        "shape": args.shape, "tile_waves": args.tile_waves,
-                       "summary_path": args.summary_path, "tile_index": args.tile_index, "build": build},
+                       "summary_path": args.summary_path, "tile_index": args.tile_index,
+                       "read_runs": args.read_runs, "build": build},
             "gbases_piled_per_s": head["gbases_piled_per_s"],
             "device_us_per_step": head["device_us_per_step"],
+            "upload_ms": head["upload_ms"],
             "kernel_us": head["kernel_us"],
             "kernels": head["kernels"],
             "parity_vs_oracle": head["parity_vs_oracle"],

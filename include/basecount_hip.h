@@ -42,7 +42,7 @@ extern "C" {
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
 #define BC_E_COMM (-5)  /* RCCL error in a multi-GPU call                                        */
 
-#define BC_ABI_VERSION 4
+#define BC_ABI_VERSION 5
 
 /* Layouts of bc_reads.seq.
  *   BC_SEQ_BAM   BAM packing: "=ACMGRSVTWYHKDBN" codes, two per byte, high nibble first
@@ -89,6 +89,11 @@ typedef struct bc_reads {
      * batches (fewer tiles than reads/16, fewer than 2^31 reads); host inputs ignore it.       */
     const int32_t* tile_reads;
     int64_t n_tiles;
+    /* Optional device run records of a sorted batch (NULL: the kernels decode the CIGARs): 4
+     * words per read, the first two aligned runs of its CIGAR as the read-chunked kernel needs
+     * them (layout in basecount_amd/csrc/bc_runs.h).  bc_reads_upload decodes every read once
+     * on the host (the same decode the kernels run) for sorted batches; host inputs ignore it. */
+    const uint32_t* read_runs;
 } bc_reads;
 
 typedef struct bc_ctx bc_ctx;

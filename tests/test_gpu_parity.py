@@ -215,6 +215,36 @@ def test_rc_pileup_after_range_error(ctx):
     assert np.array_equal(cov, ocov) and np.array_equal(ent, oent)
 
 
+@pytest.mark.parametrize("mix", ["image", "fallback", "mixed"])
+@pytest.mark.parametrize("mbq,ncols", [(0, 5), (0, 6), (20, 5)])
+def test_rc_same_without_run_records(ctx, mix, mbq, ncols):
+    """k_rc from the upload's run records (bc_reads.read_runs, the CIGARs decoded once on the
+    host) and from its own CIGAR decode: identical counts and first out-of-range read."""
+    ctx.set_shape("rc")
+    tpl = {"image": IMAGE_OK, "fallback": FALLBACK, "mixed": IMAGE_OK + FALLBACK[:2]}[mix]
+    rng = np.random.default_rng({"image": 51, "fallback": 52, "mixed": 53}[mix])
+    L = 9_000
+    b = shaped_batch(rng, L + 300, 30_000, tpl)
+    for L2 in (L + 300, L):
+        got = []
+        for use in (True, False):
+            r = D.DeviceReads(ctx, b)
+            assert r.r.read_runs
+            if not use:
+                r.r.read_runs = None
+            hist = ctx.alloc(4 * ncols * L2)
+            hist.zero()
+            ctx.count(r, L2, mbq, ncols, hist.ptr)
+            got.append((ctx.range_error(), hist.download(np.int32, ncols * L2)))
+            r.free()
+        assert got[0][0] == got[1][0]
+        assert np.array_equal(got[0][1], got[1][1])
+        exp, (br, _) = O.bcount(L2, mbq, b)
+        assert got[0][0] == br
+        if br == -1:
+            assert np.array_equal(got[0][1].reshape(ncols, L2), exp[:, :ncols].T.astype(np.int32))
+
+
 def test_rc_event_image_range_error(ctx):
     """A read running past the reference end inside an imaged chunk: the reference's first
     offending read (std::out_of_range), nothing counted past L."""

@@ -94,24 +94,33 @@ struct RcArgs {
     unsigned long long* trace;  // diagnostic only (BC_PHASE_TRACE builds): [block][wave][kRcPhases]
 };
 
-// Block-wide reduction of 8 values (max or min per slot): wave reduce, then LDS across waves.
-// Must be called by the whole block.
+// Block-wide reduction of NV <= 8 values (max or min per slot): wave reduce, then LDS across
+// waves.  Lane k of each wave stores slot k (one masked store, not one per slot); every thread
+// then reads the waves' rows as 16-byte words.  Must be called by the whole block.
 template <int NV, int NWAVES>
 __device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
+    static_assert(NV <= 8, "one 8-word row per wave");
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t mine = 0;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const uint32_t r = is_max[k] ? wave_reduce<true>(v[k]) : wave_reduce<false>(v[k]);
-        if (lane == 0) red[wave][k] = r;
+        mine = lane == k ? r : mine;
     }
+    if (lane < NV) red[wave][lane] = mine;
     __syncthreads();
+    uint32_t w[NWAVES][8];
+#pragma unroll
+    for (int q = 0; q < NWAVES; ++q) {
+        const uint4 a = *(const uint4*)&red[q][0], b = *(const uint4*)&red[q][4];
+        w[q][0] = a.x, w[q][1] = a.y, w[q][2] = a.z, w[q][3] = a.w;
+        w[q][4] = b.x, w[q][5] = b.y, w[q][6] = b.z, w[q][7] = b.w;
+    }
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-        uint32_t r = red[0][k];
-        for (int w = 1; w < NWAVES; ++w) {
-            const uint32_t o = red[w][k];
-            r = is_max[k] ? (o > r ? o : r) : (o < r ? o : r);
-        }
+        uint32_t r = w[0][k];
+#pragma unroll
+        for (int q = 1; q < NWAVES; ++q) r = is_max[k] ? (w[q][k] > r ? w[q][k] : r) : (w[q][k] < r ? w[q][k] : r);
         v[k] = r;
     }
 }
@@ -185,7 +194,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     __shared__ int32_t rpos[kRcReads];  // the chunk's read positions (window tables)
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 8 * kPadW];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
-    __shared__ uint32_t red[kRcWaves][8];
+    __shared__ __attribute__((aligned(16))) uint32_t red[kRcWaves][8];
     __shared__ uint32_t wlo[kRcWin], whi[kRcWin], wpre[kRcWin + 1];
     __shared__ uint32_t cxl[kRcReads];
     __shared__ uint32_t ncx;

@@ -20,17 +20,24 @@ constexpr uint32_t kDel = 0x80000000u;   // packed event: deletion / ref-skip
 __device__ __forceinline__ unsigned nib_col6(unsigned nib) { return (unsigned)(kNibCol6 >> (nib * 4)) & 0xFu; }
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
-// Wave-wide max / min (result in every lane's SGPR): DPP row prefix, row broadcasts, readlane.
+// Wave-wide max / min (result in every lane's SGPR): a prefix max / min within each 16-lane row
+// (DPP row_shr 1, 2, 4, 8), then the four rows' last lanes combined on the scalar unit.  The
+// DPP source's `old` operand is the operation's identity, so each step compiles to ONE fused
+// v_max/min_u32_dpp (with `old = v` the compiler keeps a separate mov + op per step: 18 VALU
+// instead of 4).
 template <bool MAX>
 __device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
+    constexpr int id = MAX ? 0 : -1;
     auto op = [](uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return op(op(r0, r1), op(r2, r3));
 }
 
 

@@ -730,17 +730,20 @@ __device__ __forceinline__ long long wave_sum_i64(long long v) {
 // Move a read cursor forward to the first index >= cur whose pos >= key (pos is sorted and the
 // keys of successive tiles increase).  `win` holds pos[wbase + lane]: the 64 reads after the
 // cursor are looked at with one ballot, refilled only when the cursor leaves them.
-__device__ __forceinline__ void advance_cursor(const int32_t* pos, int64_t n, int64_t& cur, int64_t key, int32_t& win,
-                                               int64_t& wbase, int lane) {
+// IT: the index type of reads and positions (int32_t when both fit, so the cursor arithmetic
+// stays on the scalar unit; int64_t otherwise).
+template <typename IT>
+__device__ __forceinline__ void advance_cursor(const int32_t* pos, IT n, IT& cur, IT key, int32_t& win, IT& wbase,
+                                               int lane) {
     for (;;) {
         if (cur >= n) return;
         if (cur >= wbase + 64) {
             wbase = cur;
-            const int64_t i = wbase + lane;
+            const IT i = wbase + lane;
             win = i < n ? pos[i] : INT32_MAX;
         }
-        const int below = __popcll(__ballot((int64_t)win < key));  // a prefix of the window
-        int64_t end = wbase + below;
+        const int below = __popcll(__ballot((IT)win < key));  // a prefix of the window
+        IT end = wbase + below;
         end = end < n ? end : n;
         if (end > cur) cur = end;
         if (below < 64 || cur >= n) return;
@@ -751,7 +754,7 @@ __device__ __forceinline__ void advance_cursor(const int32_t* pos, int64_t n, in
 // Sparse batches: every wave owns a contiguous run of tiles and sweeps it with two read cursors
 // (no per-tile search), walks the few reads of each tile alone, and computes the statistics of
 // its own positions in registers: no block barriers at all.  Empty tiles only store.
-template <bool QUAL, int K, bool STATS, bool SUMP>
+template <bool QUAL, int K, bool STATS, bool SUMP, typename IT>
 __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     const int lane = threadIdx.x & 63;
@@ -759,19 +762,27 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     const int nw = blockDim.x >> 6;
     uint4* myrec = (uint4*)dyn + wave * kTile * 3;
     uint8_t* mystage = dyn + (size_t)nw * kRecBytes + (size_t)wave * kStageRegion + 16;
-    const int64_t L = A.L;
+    const IT L = (IT)A.L, n = (IT)A.n;
     const int s8 = lane & 7;
     const bool qual_vec = ((uintptr_t)A.qual & 15u) == 0;
-    const int64_t G = gridDim.x;
-    const int64_t lb = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
-    const int64_t t_begin = (lb * nw + wave) * A.tiles_per_wave;
-    const int64_t t_end = t_begin + A.tiles_per_wave < A.n_tiles ? t_begin + A.tiles_per_wave : A.n_tiles;
+    const IT G = gridDim.x;
+    const IT lb = (G % 8 == 0) ? (IT)(blockIdx.x % 8) * (G / 8) + (IT)(blockIdx.x / 8) : (IT)blockIdx.x;
+    const IT tpw = (IT)A.tiles_per_wave;
+    const IT t_begin = (lb * nw + wave) * tpw;
+    const IT t_end = t_begin + tpw < (IT)A.n_tiles ? t_begin + tpw : (IT)A.n_tiles;
     if (t_begin >= t_end) return;  // no barriers in this kernel
-    int64_t lo, hi;
-    lower_bound_pair(A.pos, A.n, t_begin * kTile - A.max_span + 1, t_begin * kTile + kTile, lane, lo, hi);
-    int64_t wlo_base = lo, whi_base = hi;
-    int32_t wlo = lo + lane < A.n ? A.pos[lo + lane] : INT32_MAX;
-    int32_t whi = hi + lane < A.n ? A.pos[hi + lane] : INT32_MAX;
+    IT lo, hi;
+    {
+        int64_t l64, h64;
+        lower_bound_pair(A.pos, A.n, (int64_t)t_begin * kTile - A.max_span + 1, (int64_t)t_begin * kTile + kTile, lane,
+                         l64, h64);
+        lo = (IT)l64;
+        hi = (IT)h64;
+    }
+    IT wlo_base = lo, whi_base = hi;
+    int32_t wlo = lo + lane < n ? A.pos[lo + lane] : INT32_MAX;
+    int32_t whi = hi + lane < n ? A.pos[hi + lane] : INT32_MAX;
+    const IT max_span = (IT)A.max_span;
     // SUMP: the wave's tiles start on a quarter-buffer boundary (tiles_per_wave is a multiple of
     // 32), so it sees whole 2048-position quarters, each a subtree of numpy's pairwise tree over
     // an 8192 buffer (split evenly down to 128-element leaves): leaves of two tiles wait in LDS (16
@@ -782,13 +793,13 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + 128 * wave;
     double* mytr = myleaves + 64;  // transposition scratch of the leaf sums
     long long sum_cov = 0, sum_nz = 0;
-    for (int64_t t = t_begin; t < t_end; ++t) {
-        const int64_t t0 = t * kTile;
-        const int64_t P = t0 + lane;
+    for (IT t = t_begin; t < t_end; ++t) {
+        const IT t0 = t * kTile;
+        const IT P = t0 + lane;
         const int gb = (int)t0 + 8 * (lane >> 3);
         if (t > t_begin) {
-            advance_cursor(A.pos, A.n, lo, t0 - A.max_span + 1, wlo, wlo_base, lane);
-            advance_cursor(A.pos, A.n, hi, t0 + kTile, whi, whi_base, lane);
+            advance_cursor<IT>(A.pos, n, lo, t0 - max_span + 1, wlo, wlo_base, lane);
+            advance_cursor<IT>(A.pos, n, hi, t0 + kTile, whi, whi_base, lane);
         }
         uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
         if (hi > lo) {
@@ -809,7 +820,7 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
             int it4 = 0;
             auto chunk_nr = [&](int64_t b) { return b < hi ? (int)((hi - b) < 64 ? (hi - b) : 64) : 0; };
             ReadFields F = load_fields(A, lo, chunk_nr(lo), lane);
-            for (int64_t base = lo; base < hi; base += 64) {
+            for (int64_t base = lo; base < (int64_t)hi; base += 64) {
                 process_chunk<QUAL, K>(A, base, chunk_nr(base), F, base + 64, chunk_nr(base + 64), lane, s8, gb, t0, P,
                                        edge, beyond, bmask, myrec, mystage, qual_vec, W, it4, cnt, acc, pending, bad);
                 __builtin_amdgcn_wave_barrier();
@@ -953,10 +964,14 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         blocks = (blocks + 7) / 8 * 8;  // a multiple of the XCD count (see the kernel's tile mapping)
         const dim3 grid((unsigned)blocks), block(64 * nw);
         const size_t lds = (size_t)nw * (kRecBytes + kStageRegion) + (sump ? (size_t)nw * 128 * 8 : 0);
-#define BC_SOLO(Q, KK, ST)                                                                   \
-    do {                                                                                     \
-        if (sump) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true>), grid, block, lds, s, A); \
-        else hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST, false>), grid, block, lds, s, A);  \
+        // 32-bit reads and positions when they fit (the cursor loop then stays on the scalar unit)
+        const bool i32 = A.n < (int64_t)0x7FFFFF00 && A.n_tiles * kTile + A.max_span + 2 * kTile < (int64_t)0x7FFFFF00;
+#define BC_SOLO(Q, KK, ST)                                                                                       \
+    do {                                                                                                         \
+        if (sump && i32) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true, int32_t>), grid, block, lds, s, A); \
+        else if (sump) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true, int64_t>), grid, block, lds, s, A);   \
+        else if (i32) hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST, false, int32_t>), grid, block, lds, s, A);     \
+        else hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST, false, int64_t>), grid, block, lds, s, A);              \
     } while (0)
         if (mbq > 0) {
             if (k == 5) {

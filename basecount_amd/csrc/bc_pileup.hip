@@ -793,6 +793,36 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + 128 * wave;
     double* mytr = myleaves + 64;  // transposition scratch of the leaf sums
     long long sum_cov = 0, sum_nz = 0;
+    // SUMP: tile t's share of numpy's pairwise leaves (h: its entropies; an empty tile's are 1.0)
+    auto leaf_step = [&](IT t, bool empty, double h) {
+        if (t & 1) {
+            const double lf = (prev_empty && empty) ? 128.0
+                              : empty                 ? leaf_finish_ones(prev_empty ? 8.0 : e_prev, lane, mytr)
+                                                      : leaf_finish(prev_empty ? 8.0 : e_prev, h, lane, mytr);
+            const int leaf = (int)((t >> 1) & 15);
+            if (lane == 0) myleaves[leaf] = lf;
+            if (leaf == 15) {  // the quarter is complete: its 16 leaves, pairwise
+                __builtin_amdgcn_wave_barrier();
+                double v = myleaves[lane & 15];
+#pragma unroll
+                for (int l = 1; l < 16; l <<= 1) {  // left (lower lanes) + right
+                    const double w = __shfl_down(v, l);
+                    if ((lane & (2 * l - 1)) == 0) v = v + w;
+                }
+                const long long cs = wave_sum_i64(sum_cov), nz = wave_sum_i64(sum_nz);
+                if (lane == 0) {
+                    const int64_t q = t >> 5;
+                    A.sub_ent[q] = v;
+                    A.sub_cov[q] = cs;
+                    A.sub_nz[q] = nz;
+                }
+                sum_cov = sum_nz = 0;
+            }
+        } else {
+            prev_empty = empty;  // an empty first tile's half is 8.0 (leaf_finish_ones)
+            if (!empty) e_prev = leaf_half(h, lane, mytr);  // its half of the chains
+        }
+    };
     for (IT t = t_begin; t < t_end; ++t) {
         const IT t0 = t * kTile;
         const IT P = t0 + lane;
@@ -800,6 +830,37 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
         if (t > t_begin) {
             advance_cursor<IT>(A.pos, n, lo, t0 - max_span + 1, wlo, wlo_base, lane);
             advance_cursor<IT>(A.pos, n, hi, t0 + kTile, whi, whi_base, lane);
+        }
+        if (STATS && lo >= hi && !A.accumulate && !(BC_ABL(A) & 16)) {
+            // No read overlaps this tile, nor any tile before the next read's start tile: write
+            // that run of full tiles' constant outputs (main.py:29-53 at zero coverage) without
+            // per-tile cursor work.  The next tile with reads resumes the normal path.
+            IT nxt = t_end;
+            if (hi < n) {
+                const IT d = hi - whi_base;  // in [0, 64]: the window holds pos[whi_base ..]
+                const int32_t ph = d < 64 ? (int32_t)__builtin_amdgcn_readlane(whi, (int)d) : A.pos[hi];
+                nxt = (IT)(ph >> 6);
+            }
+            IT stop = nxt < t_end ? nxt : t_end;
+            const IT full = L / kTile;  // tiles entirely below L
+            stop = stop < full ? stop : full;
+            if (stop > t + 1) {
+                for (; t < stop; ++t) {
+                    const IT tz = t * kTile;
+#pragma unroll
+                    for (int c = 0; c < K; ++c) (A.counts + ((int64_t)c * L + tz))[lane] = 0;
+                    (A.cov + tz)[lane] = 0;
+                    if (A.pc) {
+#pragma unroll
+                        for (int j = 0; j < K; ++j) (A.pc + ((int64_t)j * L + tz))[lane] = -1.0;
+                    }
+                    (A.ent + tz)[lane] = 1.0;
+                    (A.sec + tz)[lane] = 1.0;
+                    if (SUMP && (int64_t)(tz >> 13) < A.full_chunks) leaf_step(t, true, 1.0);
+                }
+                --t;  // the loop's increment moves to `stop`
+                continue;
+            }
         }
         uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
         if (hi > lo) {
@@ -855,33 +916,7 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
                             sum_cov += cov;
                             sum_nz += cov != 0;
                         }
-                        if (t & 1) {
-                            const double lf = (prev_empty && empty) ? 128.0
-                                              : empty                 ? leaf_finish_ones(prev_empty ? 8.0 : e_prev, lane, mytr)
-                                                      : leaf_finish(prev_empty ? 8.0 : e_prev, h, lane, mytr);
-                            const int leaf = (int)((t >> 1) & 15);
-                            if (lane == 0) myleaves[leaf] = lf;
-                            if (leaf == 15) {  // the quarter is complete: its 16 leaves, pairwise
-                                __builtin_amdgcn_wave_barrier();
-                                double v = myleaves[lane & 15];
-#pragma unroll
-                                for (int l = 1; l < 16; l <<= 1) {  // left (lower lanes) + right
-                                    const double w = __shfl_down(v, l);
-                                    if ((lane & (2 * l - 1)) == 0) v = v + w;
-                                }
-                                const long long cs = wave_sum_i64(sum_cov), nz = wave_sum_i64(sum_nz);
-                                if (lane == 0) {
-                                    const int64_t q = t >> 5;
-                                    A.sub_ent[q] = v;
-                                    A.sub_cov[q] = cs;
-                                    A.sub_nz[q] = nz;
-                                }
-                                sum_cov = sum_nz = 0;
-                            }
-                        } else {
-                            prev_empty = empty;  // an empty first tile's half is 8.0 (leaf_finish_ones)
-                            if (!empty) e_prev = leaf_half(h, lane, mytr);  // its half of the chains
-                        }
+                        leaf_step(t, empty, h);
                     }
                 }
             }

@@ -483,10 +483,10 @@ else BC_WALK(4, GP, ST);                                                        
     }
 }
 
-template <bool QUAL, int K, bool STATS>
+template <bool QUAL, int K, bool STATS, typename IT>
 __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-    __shared__ int64_t rng[8][2];  // per group: the tile's read range
+    __shared__ IT rng[8][2];  // per group: the tile's read range
     if (BC_ABL(A) & 64) return;
     trace_stamp(A, 0);
     const int lane = threadIdx.x & 63;
@@ -500,27 +500,29 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
     uint32_t(*fin)[6][kTile] = (uint32_t(*)[6][kTile])(stage_all + (size_t)nw * kStageRegion);
     // aliases of the stage regions, live only after the walk (see pileup_lds_bytes)
     double* terms_g = (double*)(stage_all + (size_t)(g * S) * kStageRegion);
-    const int64_t nblk_tiles = (A.n_tiles + groups - 1) / groups;
-    const int64_t L = A.L;
+    // IT: the index type of reads, tiles and positions (int32_t when they fit: scalar math)
+    const IT n_tiles = (IT)A.n_tiles;
+    const IT nblk_tiles = (n_tiles + groups - 1) / groups;
+    const IT L = (IT)A.L;
     const int s8 = lane & 7;
     const bool qual_vec = ((uintptr_t)A.qual & 15u) == 0;
 
     // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs; give each XCD a
     // contiguous run of tiles so neighbouring tiles (which share ~2/3 of their reads) hit the
     // same L2 instead of fetching the reads' CIGAR / sequence from HBM once per tile
-    const int64_t G = gridDim.x;
-    const int64_t lb = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
-    for (int64_t bt = lb; bt < nblk_tiles; bt += G) {
-        const int64_t t = bt * groups + g;
-        const int64_t t0 = t * kTile;
-        const int64_t P = t0 + lane;
+    const IT G = gridDim.x;
+    const IT lb = (G % 8 == 0) ? (IT)(blockIdx.x % 8) * (G / 8) + (IT)(blockIdx.x / 8) : (IT)blockIdx.x;
+    for (IT bt = lb; bt < nblk_tiles; bt += G) {
+        const IT t = bt * groups + g;
+        const IT t0 = t * kTile;
+        const IT P = t0 + lane;
         const int gb = (int)t0 + 8 * (lane >> 3);  // this lane's window [gb, gb + 8)
         uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
         int64_t bad = INT64_MAX;
         // the tile's reads [lo, hi): searched by the group's first wave (the S waves would all
         // find the same range), handed to the others through LDS
-        int64_t lo = 0, hi = 0;
-        if (ws == 0 && t < A.n_tiles && !(BC_ABL(A) & 2)) {
+        IT lo = 0, hi = 0;
+        if (ws == 0 && t < n_tiles && !(BC_ABL(A) & 2)) {
 #ifdef BC_PHASE_TRACE
             if (A.trace) {  // diagnostic: latency of one dependent global load from here
                 const int32_t probe = A.pos[(lane * 1543) % (int)A.n];
@@ -539,7 +541,10 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                 lo = rg.x;
                 hi = rg.y;
             } else {
-                lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
+                int64_t l64, h64;
+                lower_bound_pair(A.pos, A.n, (int64_t)t0 - A.max_span + 1, (int64_t)t0 + kTile, lane, l64, h64);
+                lo = (IT)l64;
+                hi = (IT)h64;
             }
             trace_stamp(A, 9);
         }
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             lo = rng[g][0];
             hi = rng[g][1];
         }
-        if (t < A.n_tiles) {
+        if (t < n_tiles) {
             if (BC_ABL(A) & 1) hi = lo;
             const bool edge = t0 + kTile > L;  // uniform
             const bool beyond = P >= L;
@@ -572,14 +577,14 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
             int it4 = 0;
             uint4* myrec = rec_all + wave * kTile * 3;
             uint8_t* mystage = stage_all + (size_t)wave * kStageRegion + 16;
-            auto chunk_nr = [&](int64_t b) { return b < hi ? (int)((hi - b) < 64 ? (hi - b) : 64) : 0; };
-            int64_t base = lo + (int64_t)ws * 64;
+            auto chunk_nr = [&](IT b) { return b < hi ? (int)((hi - b) < 64 ? (hi - b) : 64) : 0; };
+            IT base = lo + (IT)ws * 64;
             ReadFields F = load_fields(A, base, chunk_nr(base), lane);
 #ifdef BC_PHASE_TRACE
             int nch = 0;
 #endif
-            for (; base < hi; base += (int64_t)S * 64) {
-                const int64_t nb = base + (int64_t)S * 64;
+            for (; base < hi; base += (IT)S * 64) {
+                const IT nb = base + (IT)S * 64;
                 process_chunk<QUAL, K>(A, base, chunk_nr(base), F, nb, chunk_nr(nb), lane, s8, gb, t0, P, edge,
                                        beyond, bmask, myrec, mystage, qual_vec, W, it4, cnt, acc, pending, bad);
                 __builtin_amdgcn_wave_barrier();
@@ -610,7 +615,7 @@ __global__ __launch_bounds__(512, 4) void k_pileup(PileArgs A) {
                 for (int c = 0; c < K; ++c) cnt[c] = fin[g][c][lane];
             }
         }
-        const bool own = t < A.n_tiles && t0 < L && !(BC_ABL(A) & 16);  // tile holds real positions
+        const bool own = t < n_tiles && t0 < L && !(BC_ABL(A) & 16);  // tile holds real positions
         if (ws == 0) {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -1045,16 +1050,21 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         if (!tbuf && hipMallocManaged((void**)&tbuf, 8 * (size_t)256 * 64 * 16 * kTracePhases) != hipSuccess) tbuf = nullptr;
         if (tn <= (size_t)256 * 64 * 16 * kTracePhases) A.trace = tbuf;
     }
+    // 32-bit reads, tiles and positions when they fit
+    const bool i32 = A.n < (int64_t)0x7FFFFF00 && A.n_tiles * kTile + A.max_span + 2 * kTile < (int64_t)0x7FFFFF00;
     // > 64 KiB of dynamic LDS must be allowed per kernel (160 KiB per CU on gfx950)
 #define BC_PILE(Q, KK, ST)                                                                                   \
     do {                                                                                                     \
         static bool attr_set = false;                                                                        \
         if (!attr_set) {                                                                                     \
-            (void)hipFuncSetAttribute((const void*)k_pileup<Q, KK, ST>,                                      \
+            (void)hipFuncSetAttribute((const void*)k_pileup<Q, KK, ST, int32_t>,                             \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);        \
+            (void)hipFuncSetAttribute((const void*)k_pileup<Q, KK, ST, int64_t>,                             \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);        \
             attr_set = true;                                                                                 \
         }                                                                                                    \
-        hipLaunchKernelGGL((k_pileup<Q, KK, ST>), grid, block, lds, s, A);                                   \
+        if (i32) hipLaunchKernelGGL((k_pileup<Q, KK, ST, int32_t>), grid, block, lds, s, A);                 \
+        else hipLaunchKernelGGL((k_pileup<Q, KK, ST, int64_t>), grid, block, lds, s, A);                     \
         if (A.trace && ++tcalls == 20) {                                                                     \
             (void)hipStreamSynchronize(s);                                                                   \
             if (FILE* f = std::fopen(tpath, "wb")) {                                                         \

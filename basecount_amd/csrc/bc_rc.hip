@@ -486,15 +486,59 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     img[tid * kImgRows + row] = x;
                 }
             };
+            // Interior rows, then boundary rows.  A row that no boundary (Z, B0, A1, SP) falls
+            // strictly inside lies entirely in one segment (run 0, the deletions, run 1) or
+            // outside the read, so its word is one stream word, kClsDel or 0: the loop takes it
+            // from per-lane row bitmasks (one v_bfe_i32 per row and segment) instead of four
+            // clamped masks.  The <= 4 rows a boundary cuts are then overwritten with the exact
+            // formula above, at their (per-lane) row.
+            auto rowmask = [](int a, int b) -> uint32_t {  // rows lying entirely in stream bits [a, b)
+                const int lo = (a + 31) >> 5, hi = b >> 5;
+                return hi > lo ? lo32_bit(hi) - lo32_bit(lo) : 0u;
+            };
+            auto interior = [&]() {
+                const uint32_t o0 = rowmask(Z, B0e), o1 = rowmask(A1, SP);
+                uint32_t p0 = w0[0], p1 = w1[0];
+#pragma unroll
+                for (int row = 0; row < kImgRows; ++row) {
+                    if (row >= kImgRows - 4 && row >= NWc) continue;  // (uniform) past the chunk
+                    const uint32_t n0 = w0[row + 1], n1 = w1[row + 1];
+                    const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)o0, row, 1);
+                    const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)o1, row, 1);
+                    const uint32_t x1 = __builtin_amdgcn_alignbit(n1, p1, sh1) & m1;
+                    // (s0 & m0) | x1: a row lies in at most one segment
+                    img[tid * kImgRows + row] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n0, p0, sh0), m0, x1, 0xEA);
+                    p0 = n0;
+                    p1 = n1;
+                }
+                // rows lying entirely in a deletion (>= 8 deleted positions; none in most waves)
+                for (uint32_t od = rowmask(B0e, A1); od; od &= od - 1u) img[tid * kImgRows + __builtin_ctz(od)] = kClsDel;
+                auto fix = [&](int b) {  // the row boundary b cuts, exactly
+                    const int rb = b >> 5;
+                    if ((b & 31) == 0 || rb >= kImgRows) return;
+                    const int lo = 32 * rb;
+                    auto ge = [&](int Y) {
+                        const int d = Y - lo;
+                        return (uint32_t)shl64_mod64(0xFFFFFFFFull, d < 0 ? 0 : (d > 32 ? 32 : d));
+                    };
+                    const uint32_t gz = ge(Z), gb = ge(B0e), ga = ge(A1), gs = ge(SP);
+                    const uint32_t x0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(w0[rb + 1], w0[rb], sh0), gz, gb, 0x40);
+                    const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(w1[rb + 1], w1[rb], sh1), ga, gs, 0x40);
+                    img[tid * kImgRows + rb] =
+                        __builtin_amdgcn_bitop3_b32(x0, x1, __builtin_amdgcn_bitop3_b32(kClsDel, gb, ga, 0x40), 0xFE);
+                };
+                fix(Z);
+                fix(B0e);
+                fix(A1);
+                fix(SP);
+            };
             if (!simple || (BC_ABL(A) & 16384)) {
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) img[tid * kImgRows + row] = 0u;
             } else if (8 * (int64_t)(G0 + kImgRows) > A.L) {  // (uniform) rows may reach past L
                 expand(std::true_type{}, std::true_type{});
-            } else if (maxrun == 2) {
-                expand(std::true_type{}, std::false_type{});
             } else {
-                expand(std::false_type{}, std::false_type{});
+                interior();
             }
         }
         pf_ok = false;

@@ -245,6 +245,35 @@ def test_rc_same_without_run_records(ctx, mix, mbq, ncols):
             assert np.array_equal(got[0][1].reshape(ncols, L2), exp[:, :ncols].T.astype(np.int32))
 
 
+IMAGE_DEEP = IMAGE_OK + [[(0, 50), (2, 20), (0, 80)], [(0, 40), (3, 41), (0, 60)],
+                         [(4, 3), (0, 31), (2, 9), (0, 90), (4, 2)], [(0, 32), (2, 32), (0, 64)],
+                         [(0, 1), (2, 100), (0, 1)], [(0, 8)], [(0, 63), (1, 9), (0, 64)]]
+
+
+@pytest.mark.parametrize("mbq,ncols", [(0, 5), (0, 6), (20, 5)])
+def test_rc_event_image_deep(ctx, mbq, ncols):
+    """Deep batches whose 256-read chunks fit the event image (<= 23 windows): one- and two-run
+    reads, deletions and reference skips that cover whole image rows, boundaries on and off
+    the rows' 8-position edges; with and without the upload's run records."""
+    ctx.set_shape("rc")
+    rng = np.random.default_rng(35 + mbq + ncols)
+    L = 3_000
+    b = shaped_batch(rng, L, 150_000, IMAGE_DEEP)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    for use_runs in (True, False):
+        r = D.DeviceReads(ctx, b)
+        if not use_runs:
+            r.r.read_runs = None
+        hist = ctx.alloc(4 * ncols * L)
+        hist.zero()
+        ctx.count(r, L, mbq, ncols, hist.ptr)
+        assert ctx.range_error() == -1
+        got = hist.download(np.int32, ncols * L).reshape(ncols, L)
+        r.free()
+        assert np.array_equal(got, exp[:, :ncols].T.astype(np.int32)), use_runs
+
+
 def test_rc_event_image_range_error(ctx):
     """A read running past the reference end inside an imaged chunk: the reference's first
     offending read (std::out_of_range), nothing counted past L."""

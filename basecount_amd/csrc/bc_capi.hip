@@ -120,12 +120,38 @@ std::vector<int32_t> tile_index(const bc_reads& h, int sorted, int max_span, int
 }
 
 // bc_reads.read_runs for a sorted batch: every read's CIGAR decoded once (bc::decode_runs, the
-// kernels' own decode) into its 16-byte run record, on up to 16 host threads.
-std::vector<uint32_t> read_runs(const bc_reads& h, int sorted) {
+// kernels' own decode) into its 16-byte run record, then per 256-read chunk of k_rc the bounds
+// its block would otherwise reduce at the start of the chunk (chunk_summary), on up to 16 host
+// threads.  *chunks = the number of summaries after the n records.
+void chunk_summary(const bc_reads& h, const uint32_t* rec, int64_t c0, int64_t c1, uint32_t* s) {
+    uint32_t p0 = 0xFFFFFFFFu, p1 = 0, slo = 0xFFFFFFFFu, shi = 0, msp = 0, mrun = 0, gap = 0;
+    for (int64_t i = c0; i < c1; ++i) {  // the kernel's per-thread values, reduced (bc_rc.hip)
+        const uint32_t* q = rec + 4 * i;
+        const bc::RunTable T = bc::unpack_runs(q[0], q[1], q[2], q[3]);
+        const uint32_t pos = (uint32_t)h.pos[i], msn = h.seq_nib[i];
+        const uint32_t span = T.complex ? bc::full_span(h.cigar + h.cig_beg[i], h.cig_n[i]) : T.span;
+        p0 = std::min(p0, pos);
+        p1 = std::max(p1, pos + span);
+        if (T.complex) continue;
+        if (T.qlen) {
+            slo = std::min(slo, msn >> 1);
+            shi = std::max(shi, (msn + T.qlen + 1) >> 1);
+        }
+        msp = std::max(msp, T.span);
+        mrun = std::max(mrun, bc::run_shape(T));
+        gap |= T.gap ? 1u : 0u;
+    }
+    const uint32_t v[8] = {p0, p1, slo, shi, msp, mrun, gap, 0u};
+    std::memcpy(s, v, sizeof v);
+}
+std::vector<uint32_t> read_runs(const bc_reads& h, int sorted, int32_t* chunks) {
     std::vector<uint32_t> out;
+    *chunks = 0;
     const int64_t n = h.n_reads;
     if (!sorted || n <= 0) return out;
-    out.resize((size_t)n * 4);
+    const int64_t nch = (n + bc::kRcChunkReads - 1) / bc::kRcChunkReads;
+    const bool sums = nch < (int64_t)0x7FFFFFFF;
+    out.resize((size_t)n * 4 + (sums ? (size_t)nch * 8 : 0));
     auto work = [&](int64_t i0, int64_t i1) {
         for (int64_t i = i0; i < i1; ++i) {
             const uint32_t cn = h.cig_n[i];
@@ -135,15 +161,27 @@ std::vector<uint32_t> read_runs(const bc_reads& h, int sorted) {
             bc::pack_runs(bc::decode_runs<2>(w, cn, c), &out[(size_t)i * 4]);
         }
     };
+    auto sum = [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; ++k)
+            chunk_summary(h, out.data(), k * bc::kRcChunkReads, std::min<int64_t>(n, (k + 1) * bc::kRcChunkReads),
+                          &out[(size_t)n * 4 + (size_t)k * 8]);
+    };
     const unsigned hw = std::thread::hardware_concurrency();
     const int64_t nt = std::min<int64_t>({(int64_t)(hw ? hw : 1), 16, (n + 65535) / 65536});
     if (nt <= 1) {
         work(0, n);
-        return out;
+        if (sums) sum(0, nch);
+    } else {
+        std::vector<std::thread> th;
+        for (int64_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+        for (auto& x : th) x.join();
+        th.clear();
+        if (sums) {
+            for (int64_t t = 0; t < nt; ++t) th.emplace_back(sum, nch * t / nt, nch * (t + 1) / nt);
+            for (auto& x : th) x.join();
+        }
     }
-    std::vector<std::thread> th;
-    for (int64_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
-    for (auto& x : th) x.join();
+    if (sums) *chunks = (int32_t)nch;
     return out;
 }
 
@@ -378,7 +416,8 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     // 64-position tile, so the tiled kernel starts each tile with one load instead of a search
     std::vector<int32_t> tidx = tile_index(*h, d->sorted, d->max_span, d->max_end);
     // the run records of a sorted batch (bc_reads.read_runs): its CIGARs decoded once, here
-    std::vector<uint32_t> runs = read_runs(*h, d->sorted);
+    int32_t run_chunks = 0;
+    std::vector<uint32_t> runs = read_runs(*h, d->sorted, &run_chunks);
     constexpr int kArr = 9;
     void* p[kArr] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // the sequence buffer is sized for BC_SEQ_EVENT (converted in place after the copy)
@@ -426,6 +465,7 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     d->tile_reads = (const int32_t*)p[7];
     d->n_tiles = (int64_t)tidx.size() / 2;
     d->read_runs = (const uint32_t*)p[8];
+    d->run_chunks = run_chunks;
     d->seq_layout = BC_SEQ_EVENT;
     HIP_TRY(hipStreamSynchronize(c->stream));  // also keeps tidx / runs alive until their copies are done
     return BC_OK;

@@ -45,6 +45,7 @@ constexpr int kImgRows = 23;  // windows an imaged chunk may cover (odd: the ima
 constexpr int kPadW = 24;     // stage pad words on each side (kImgRows + 1, see the image expansion)
 constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's first base
 #include "bc_walk.h"
+static_assert(kRcChunk == kRcChunkReads, "the upload summarises chunks of k_rc's size (bc_runs.h)");
 
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
 constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
@@ -87,6 +88,7 @@ struct RcArgs {
     int64_t qual_bytes;
     int64_t n_chunks;
     const uint4* runs;  // bc_reads.read_runs (run records, bc_runs.h) or NULL: decode the CIGARs
+    const uint4* sums;  // the upload's chunk summaries (2 x uint4 per chunk, after the records) or NULL
     int32_t* counts;  // [ncols][L], accumulated into
     unsigned long long* err;
     int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events,
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t red[kRcWaves][8];
     __shared__ uint32_t wlo[kRcWin], whi[kRcWin], wpre[kRcWin + 1];
     __shared__ uint32_t cxl[kRcReads];
-    __shared__ uint32_t ncx;
+    __shared__ uint32_t ncx[2];  // complex reads of the chunk (by chunk parity: no barrier to reset)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, s8 = lane & 7;
     uint8_t* stage = stage_raw + 4 * kPadW;
@@ -227,6 +229,11 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // registers (the others spill with the extra path)
     constexpr bool kRunsOn = !QUAL && NC == 5;
     const uint4* const runs = kRunsOn ? A.runs : nullptr;
+    // the upload's chunk summaries: the chunk bounds without the block reduction (and its barrier)
+    const uint4* const sums = kRunsOn && A.runs ? A.sums : nullptr;
+    if (tid < 2) ncx[tid] = 0;
+    __syncthreads();
+    int par = 0;                // chunk parity (ncx slot)
     constexpr int kPf = 6;
     uint32_t pw[kPf] = {0u, 0u, 0u, 0u, 0u, 0u};
     bool pf_ok = false;
@@ -318,11 +325,11 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         }
         const bool cx = valid && T.complex;
         const bool simple = valid && !cx;
-        if (tid == 0) ncx = 0;
+        if (tid == 0) ncx[par ^ 1] = 0;  // the next chunk's slot (last read before the previous end barrier)
         // chunk bounds: P0 / P1 over all reads (complex ones: their true span), sequence segment
         // and maxima over the simple reads
         uint32_t cspan = T.span;
-        if (cx) {
+        if (cx && !sums) {
             uint64_t sp = 0;
             for (uint32_t k = 0; k < mcn; ++k) {
                 const uint32_t wk = A.cigar[mcb + k];
@@ -330,23 +337,28 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             }
             cspan = sp > 0x3FFFFFFFu ? 0x3FFFFFFFu : (uint32_t)sp;
         }
-        uint32_t v[7] = {valid ? mpos : 0xFFFFFFFFu,
-                         valid ? mpos + cspan : 0u,
-                         (simple && T.qlen) ? (msn >> 1) : 0xFFFFFFFFu,
-                         (simple && T.qlen) ? ((msn + T.qlen + 1) >> 1) : 0u,
-                         simple ? T.span : 0u,
-                         // reads the event image cannot take (first run not at the read start, last
-                         // run not at its end) count as 3 runs: such a chunk takes the run tables
-                         simple ? ((T.nrun >= 1 && T.st[0] == 0u &&
-                                    (T.nrun == 1 ? T.en[0] : T.en[1]) == T.span) || T.nrun > 2
-                                       ? (uint32_t)T.nrun
-                                       : 3u)
-                                : 0u,
-                         (simple && T.gap) ? 1u : 0u};
-        const bool is_max[7] = {false, true, false, true, true, true, true};
-        RC_STAMP(1);
-        block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
-        RC_STAMP(2);
+        uint32_t v[7];
+        if (sums) {  // (uniform) reduced by the upload (bc_capi.hip chunk_summary: the same values)
+            const uint4 s0 = sums[2 * chunk], s1 = sums[2 * chunk + 1];
+            v[0] = U(s0.x), v[1] = U(s0.y), v[2] = U(s0.z), v[3] = U(s0.w);
+            v[4] = U(s1.x), v[5] = U(s1.y), v[6] = U(s1.z);
+            RC_STAMP(1);
+            RC_STAMP(2);
+        } else {
+            v[0] = valid ? mpos : 0xFFFFFFFFu;
+            v[1] = valid ? mpos + cspan : 0u;
+            v[2] = (simple && T.qlen) ? (msn >> 1) : 0xFFFFFFFFu;
+            v[3] = (simple && T.qlen) ? ((msn + T.qlen + 1) >> 1) : 0u;
+            v[4] = simple ? T.span : 0u;
+            // reads the event image cannot take (first run not at the read start, last run not
+            // at its end) count as 3 runs: such a chunk takes the run tables
+            v[5] = simple ? run_shape(T) : 0u;
+            v[6] = (simple && T.gap) ? 1u : 0u;
+            const bool is_max[7] = {false, true, false, true, true, true, true};
+            RC_STAMP(1);
+            block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
+            RC_STAMP(2);
+        }
         const int64_t P0 = v[0], P1 = v[1];
         uint32_t seg_lo = v[2];
         const uint32_t seg_hi = v[3];
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const bool gap = v[6] != 0;
         if (maxrun > 2) decode(std::integral_constant<int, kMaxRuns>{});  // (uniform) full run tables
         seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
-        if (cx) cxl[atomicAdd(&ncx, 1u)] = (uint32_t)tid;
+        if (cx) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
         if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
         const bool staged = spec_ok || seg_hi - seg_lo <= (uint32_t)kStage;
@@ -770,10 +782,11 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             __syncthreads();  // hist reused by the next pass / chunk
         }
         // ---- complex reads: one wave per read, global atomics
-        const uint32_t nc = U(ncx);
+        const uint32_t nc = U(ncx[par]);
         for (uint32_t q = wave; q < nc; q += kRcWaves) rc_complex<QUAL, NC>(A, c0 + cxl[q], bad);
         __syncthreads();  // records / stage / cxl reused by the next chunk
         RC_STAMP(6);
+        par ^= 1;
     }
 #ifdef BC_PHASE_TRACE
     if (A.trace && lane == 0)
@@ -826,6 +839,7 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
 #endif
     constexpr int nt = kRcChunk;
     A.n_chunks = (r.n_reads + nt - 1) / nt;
+    A.sums = A.runs && r.run_chunks == A.n_chunks ? A.runs + r.n_reads : nullptr;
     // resident blocks: LDS bounds a CU to 3 (event image + stage + histogram)
     const int64_t cap = 256 * 3;
     const int64_t blocks = A.n_chunks < cap ? A.n_chunks : cap;

@@ -113,3 +113,24 @@ BC_HD RunTable unpack_runs(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     T.qlen = w >> 16;
     return T;
 }
+
+// ---- chunk summaries of the read-chunked kernel (bc_reads.read_runs after the records) ----
+constexpr int kRcChunkReads = 256;  // reads per k_rc chunk (one per thread of its block)
+
+// A simple read's run shape for k_rc: its run count when the event image can take it (first run
+// at the read start, last run at its end) or when it has more than two runs, else 3 (a chunk
+// holding such a read walks the run tables).
+BC_HD uint32_t run_shape(const RunTable& T) {
+    return ((T.nrun >= 1 && T.st[0] == 0u && (T.nrun == 1 ? T.en[0] : T.en[1]) == T.span) || T.nrun > 2)
+               ? (uint32_t)T.nrun
+               : 3u;
+}
+
+// A complex read's reference span (M/=/X/D/N), capped at 2^30 - 1.
+BC_HD uint32_t full_span(const uint32_t* cg, uint32_t cn) {
+    uint64_t sp = 0;
+    for (uint32_t k = 0; k < cn; ++k)
+        if (mlike(cg[k] & 15u) || dlike(cg[k] & 15u)) sp += cg[k] >> 4;
+    return sp > 0x3FFFFFFFu ? 0x3FFFFFFFu : (uint32_t)sp;
+}
+

@@ -39,7 +39,7 @@ class BcReads(C.Structure):
         ("max_span", C.c_int32),
         ("max_end", C.c_int64),
         ("seq_layout", C.c_int32),  # BC_SEQ_BAM 0 / BC_SEQ_EVENT 1
-        ("reserved", C.c_int32),
+        ("run_chunks", C.c_int32),
         ("tile_reads", C.c_void_p),  # optional per-tile read ranges (bc_reads_upload)
         ("n_tiles", C.c_int64),
         ("read_runs", C.c_void_p),  # optional run records, 4 words per read (bc_reads_upload)

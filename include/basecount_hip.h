@@ -42,7 +42,7 @@ extern "C" {
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
 #define BC_E_COMM (-5)  /* RCCL error in a multi-GPU call                                        */
 
-#define BC_ABI_VERSION 5
+#define BC_ABI_VERSION 6
 
 /* Layouts of bc_reads.seq.
  *   BC_SEQ_BAM   BAM packing: "=ACMGRSVTWYHKDBN" codes, two per byte, high nibble first
@@ -81,7 +81,7 @@ typedef struct bc_reads {
     int32_t max_span;         /* upper bound of every read's reference span (M/D/N/=/X bases)  */
     int64_t max_end;          /* upper bound of pos[i] + span[i] over the batch                */
     int32_t seq_layout;       /* BC_SEQ_BAM or BC_SEQ_EVENT                                    */
-    int32_t reserved;         /* 0                                                             */
+    int32_t run_chunks;       /* chunk summaries after the run records (see read_runs), or 0   */
     /* Optional device index of a sorted batch (NULL / 0: the tiled kernel searches pos[]).  For
      * the 64-position tile t < n_tiles, tile_reads[2t] and tile_reads[2t+1] are the reads
      * [lo, hi) that can overlap it: lo = first i with pos[i] > 64t - max_span, hi = first i with
@@ -92,7 +92,11 @@ typedef struct bc_reads {
     /* Optional device run records of a sorted batch (NULL: the kernels decode the CIGARs): 4
      * words per read, the first two aligned runs of its CIGAR as the read-chunked kernel needs
      * them (layout in basecount_amd/csrc/bc_runs.h).  bc_reads_upload decodes every read once
-     * on the host (the same decode the kernels run) for sorted batches; host inputs ignore it. */
+     * on the host (the same decode the kernels run) for sorted batches; host inputs ignore it.
+     * When run_chunks > 0, read_runs[4 n_reads ..] then holds run_chunks summaries of 8 words,
+     * one per 256 consecutive reads (the read-chunked kernel's chunk): min start, max end,
+     * first / last-plus-one byte of their aligned sequence, max span, a run-shape code and a
+     * deletion flag over the reads with simple CIGARs (bc_runs.h: chunk_summary).              */
     const uint32_t* read_runs;
 } bc_reads;
 

@@ -254,16 +254,20 @@ IMAGE_DEEP = IMAGE_OK + [[(0, 50), (2, 20), (0, 80)], [(0, 40), (3, 41), (0, 60)
 def test_rc_event_image_deep(ctx, mbq, ncols):
     """Deep batches whose 256-read chunks fit the event image (<= 23 windows): one- and two-run
     reads, deletions and reference skips that cover whole image rows, boundaries on and off
-    the rows' 8-position edges; with and without the upload's run records."""
+    the rows' 8-position edges; with the upload's run records and chunk summaries, with the
+    records only, and from the CIGARs."""
     ctx.set_shape("rc")
     rng = np.random.default_rng(35 + mbq + ncols)
     L = 3_000
     b = shaped_batch(rng, L, 150_000, IMAGE_DEEP)
     exp, (br, _) = O.bcount(L, mbq, b)
     assert br == -1
-    for use_runs in (True, False):
+    for mode in ("records+summaries", "records", "cigars"):
         r = D.DeviceReads(ctx, b)
-        if not use_runs:
+        assert r.r.read_runs and r.r.run_chunks == (len(b["pos"]) + 255) // 256
+        if mode != "records+summaries":
+            r.r.run_chunks = 0  # the block reduces the chunk bounds itself
+        if mode == "cigars":
             r.r.read_runs = None
         hist = ctx.alloc(4 * ncols * L)
         hist.zero()
@@ -271,7 +275,7 @@ def test_rc_event_image_deep(ctx, mbq, ncols):
         assert ctx.range_error() == -1
         got = hist.download(np.int32, ncols * L).reshape(ncols, L)
         r.free()
-        assert np.array_equal(got, exp[:, :ncols].T.astype(np.int32)), use_runs
+        assert np.array_equal(got, exp[:, :ncols].T.astype(np.int32)), mode
 
 
 def test_rc_event_image_range_error(ctx):

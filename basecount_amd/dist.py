@@ -100,10 +100,19 @@ def _recv_exact(s: socket.socket, n: int) -> bytes:
     return buf
 
 
-def rendezvous_id(rank: int, world: int, make_id, timeout: float = 300.0) -> bytes:
-    """Rank 0 calls make_id() and sends the bytes to every other rank over TCP."""
+def _rdzv_timeout() -> float:
+    v = os.environ.get("BASECOUNT_RDZV_TIMEOUT")
+    return float(v) if v else 120.0
+
+
+def rendezvous_id(rank: int, world: int, make_id, timeout: float | None = None) -> bytes:
+    """Rank 0 calls make_id() and sends the bytes to every other rank over TCP (port
+    ``BASECOUNT_RDZV_PORT``, default MASTER_PORT + 1).  The other ranks retry the connection
+    for ``timeout`` seconds (``BASECOUNT_RDZV_TIMEOUT``, default 120); rank 0 fails at once,
+    with the port in the message, if the port is taken."""
     addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = _rdzv_port()
+    timeout = _rdzv_timeout() if timeout is None else float(timeout)
     deadline = time.monotonic() + timeout
     if rank == 0:
         uid = make_id()
@@ -111,7 +120,12 @@ def rendezvous_id(rank: int, world: int, make_id, timeout: float = 300.0) -> byt
             return uid
         srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-        srv.bind((addr, port))
+        try:
+            srv.bind((addr, port))
+        except OSError as e:
+            srv.close()
+            raise RuntimeError(f"rank 0 cannot bind the rendezvous port {addr}:{port} ({e}); set "
+                               "BASECOUNT_RDZV_PORT to a free port") from e
         srv.listen(max(1, world))
         srv.settimeout(timeout)
         try:
@@ -129,9 +143,10 @@ def rendezvous_id(rank: int, world: int, make_id, timeout: float = 300.0) -> byt
                 s.sendall(struct.pack("<I", rank))
                 (n,) = struct.unpack("<I", _recv_exact(s, 4))
                 return _recv_exact(s, n)
-        except (ConnectionRefusedError, socket.timeout, OSError):
+        except (ConnectionRefusedError, socket.timeout, OSError) as e:
             if time.monotonic() > deadline:
-                raise
+                raise RuntimeError(f"rank {rank}: no rendezvous from rank 0 at {addr}:{port} within "
+                                   f"{timeout:.0f} s (BASECOUNT_RDZV_TIMEOUT)") from e
             time.sleep(0.05)
 
 

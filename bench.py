@@ -531,9 +531,76 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     return res
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as torchrun would), relay rank
+    0's stdout (the JSON line), send the other ranks' stdout to stderr, and return non-zero if
+    any rank fails (the others are then stopped).  The parent never touches the GPU: it only
+    starts processes (nothing here imports the HIP library)."""
+    import signal
+    import subprocess
+
+    master, rdzv = _free_port(), _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master), BASECOUNT_RDZV_PORT=str(rdzv))
+        out = None if r == 0 else sys.stderr.fileno()
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, stdout=out))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    deadline = time.monotonic() + 30.0  # let the others report their own errors
+                    for q in live:
+                        while q.poll() is None and time.monotonic() < deadline:
+                            time.sleep(0.1)
+                        if q.poll() is None:
+                            q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
+
+
+def launch_check(world: int, rank: int) -> None:
+    """``--launch-check``: the launch path alone, no GPU (CPU tests of the spawner): every rank
+    joins the job's process group and rank 0 prints the ranks it sees."""
+    from basecount_amd.dist import Group
+
+    group = Group()
+    ranks = [v[0] for v in group.all_gather_ints([rank])]
+    pids = [v[0] for v in group.all_gather_ints([os.getpid()])]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks": ranks, "pids": pids, "comm": group.backend}), flush=True)
+    group.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and join their process group only (no GPU work)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
@@ -560,9 +627,19 @@ def main():
                     help="run a diagnostic (BC_DIAG) build; its numbers are marked as such")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process starts the N ranks itself (before anything touches the GPU)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
+    if args.launch_check:
+        launch_check(world, rank)
+        return
 
     from basecount_amd import device as D
     from basecount_amd.main import context

@@ -115,6 +115,18 @@ def bcio() -> C.CDLL:
     lib.bcio_ref_len.restype = C.c_int64
     lib.bcio_get_records.argtypes = [C.c_void_p, C.POINTER(BcioRecords)]
     lib.bcio_select.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(BcioSelection)]
+    lib.bcio_stream_open.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
+    lib.bcio_stream_next.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_void_p)]
+    lib.bcio_stream_records.argtypes = [C.c_void_p]
+    lib.bcio_stream_records.restype = C.c_int64
+    lib.bcio_stream_n_refs.argtypes = [C.c_void_p]
+    lib.bcio_stream_n_refs.restype = C.c_int32
+    lib.bcio_stream_ref_name.argtypes = [C.c_void_p, C.c_int32]
+    lib.bcio_stream_ref_name.restype = C.c_char_p
+    lib.bcio_stream_ref_len.argtypes = [C.c_void_p, C.c_int32]
+    lib.bcio_stream_ref_len.restype = C.c_int64
+    lib.bcio_stream_close.argtypes = [C.c_void_p]
+    lib.bcio_stream_close.restype = None
     lib.bcio_write_bam.argtypes = [C.c_char_p, C.POINTER(BcioWriteSpec)]
     lib.bcio_seq_to_event.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int]
     lib.bcio_fmt_new.argtypes = [C.POINTER(C.c_void_p)]
@@ -124,7 +136,6 @@ def bcio() -> C.CDLL:
         C.c_void_p, C.c_char_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
         C.c_void_p, C.c_int, C.c_int, C.c_int,
     ]
-    lib.bcio_fmt_take.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_int64)]
     lib.bcio_fmt_take.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
     lib.bcio_fmt_pyround_float.argtypes = [C.c_double, C.c_int, C.c_char_p, C.c_int]
     lib.bcio_fmt_pyround_int.argtypes = [C.c_int64, C.c_int, C.c_char_p, C.c_int]

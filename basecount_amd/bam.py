@@ -54,16 +54,21 @@ class Selection:
 
 
 class BamFile:
-    """A fully decoded BAM file (records in file order)."""
+    """A fully decoded BAM file (records in file order), or one batch of a BamStream (then its
+    record indices count from the batch's first record, ``first_record`` in the file)."""
 
-    def __init__(self, path: str, nthreads: int = 0):
+    def __init__(self, path: str | None, nthreads: int = 0, *, _handle=None, _first: int = 0):
         lib = N.bcio()
-        h = C.c_void_p()
-        rc = lib.bcio_open(os.fsencode(path), int(nthreads), C.byref(h))
-        if rc == -1:
-            raise FileNotFoundError(lib.bcio_last_error().decode())
-        N.bcio_check(rc)
+        if _handle is None:
+            h = C.c_void_p()
+            rc = lib.bcio_open(os.fsencode(path), int(nthreads), C.byref(h))
+            if rc == -1:
+                raise FileNotFoundError(lib.bcio_last_error().decode())
+            N.bcio_check(rc)
+        else:
+            h = _handle
         self._h = h
+        self.first_record = int(_first)
         nr = lib.bcio_n_refs(h)
         self.references = tuple(lib.bcio_ref_name(h, i).decode() for i in range(nr))
         self.lengths = tuple(int(lib.bcio_ref_len(h, i)) for i in range(nr))
@@ -166,6 +171,70 @@ class BamFile:
         j = base_nib + idx
         byte = self.seq[j >> 1]
         return np.where(j & 1, byte & 0xF, byte >> 4)
+
+
+class BamStream:
+    """A BAM file decoded in batches of records (file order) with bounded memory: the
+    reference's chunked read loop (main.py:142-162) without holding the file.
+
+        with BamStream(path) as s:
+            for batch in s.batches(1_000_000):   # BamFile per batch, closed when the next comes
+                ...
+    """
+
+    def __init__(self, path: str, nthreads: int = 0):
+        lib = N.bcio()
+        h = C.c_void_p()
+        rc = lib.bcio_stream_open(os.fsencode(path), int(nthreads), C.byref(h))
+        if rc == -1:
+            raise FileNotFoundError(lib.bcio_last_error().decode())
+        N.bcio_check(rc)
+        self._h = h
+        nr = lib.bcio_stream_n_refs(h)
+        self.references = tuple(lib.bcio_stream_ref_name(h, i).decode() for i in range(nr))
+        self.lengths = tuple(int(lib.bcio_stream_ref_len(h, i)) for i in range(nr))
+
+    def next_batch(self, max_records: int) -> BamFile | None:
+        lib = N.bcio()
+        first = int(lib.bcio_stream_records(self._h))
+        out = C.c_void_p()
+        N.bcio_check(lib.bcio_stream_next(self._h, int(max_records), C.byref(out)))
+        if not out.value:
+            return None
+        return BamFile(None, _handle=out, _first=first)
+
+    def batches(self, max_records: int):
+        """Yield the batches; each is closed when the next one is requested."""
+        prev = None
+        try:
+            while True:
+                b = self.next_batch(max_records)
+                if prev is not None:
+                    prev.close()
+                prev = b
+                if b is None:
+                    return
+                yield b
+        finally:
+            if prev is not None:
+                prev.close()
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            N.bcio().bcio_stream_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def write_bam(path, references, lengths, tid, pos, flag, mapq, cig_off, cigar, l_seq, seq_off,

@@ -11,12 +11,6 @@
 
 #include "bc_internal.h"
 
-namespace bc {
-namespace {
-#include "bc_runs.h"
-}  // namespace
-}  // namespace bc
-
 namespace {
 
 thread_local std::string g_err;
@@ -99,90 +93,13 @@ std::pair<int, int64_t> host_spans(const bc_reads& r) {
     return {(int)std::min<uint64_t>(best, 0x7fffffff), end};
 }
 
-// bc_reads.tile_reads for a sorted batch with fewer 64-position tiles (up to max_end) than
-// reads / 16 and fewer than 2^31 reads, else empty: per tile t, [lo, hi) = the reads with
-// 64t - max_span < pos < 64t + 64, the range the tiled kernel otherwise searches for
-// (lower_bound_pair in bc_pileup.hip).  Two monotone cursors: O(reads + tiles).
-std::vector<int32_t> tile_index(const bc_reads& h, int sorted, int max_span, int64_t max_end) {
-    std::vector<int32_t> out;
-    const int64_t n = h.n_reads, tiles = (max_end + 63) / 64;
-    if (!sorted || n <= 0 || n >= (int64_t)0x7FFFFFC0 || tiles <= 0 || tiles > n / 16) return out;
-    out.resize((size_t)tiles * 2);
-    int64_t lo = 0, hi = 0;
-    for (int64_t t = 0; t < tiles; ++t) {
-        const int64_t vlo = 64 * t - max_span + 1, vhi = 64 * t + 64;
-        while (lo < n && (int64_t)h.pos[lo] < vlo) ++lo;
-        while (hi < n && (int64_t)h.pos[hi] < vhi) ++hi;
-        out[2 * t] = (int32_t)lo;
-        out[2 * t + 1] = (int32_t)hi;
-    }
-    return out;
-}
-
-// bc_reads.read_runs for a sorted batch: every read's CIGAR decoded once (bc::decode_runs, the
-// kernels' own decode) into its 16-byte run record, then per 256-read chunk of k_rc the bounds
-// its block would otherwise reduce at the start of the chunk (chunk_summary), on up to 16 host
-// threads.  *chunks = the number of summaries after the n records.
-void chunk_summary(const bc_reads& h, const uint32_t* rec, int64_t c0, int64_t c1, uint32_t* s) {
-    uint32_t p0 = 0xFFFFFFFFu, p1 = 0, slo = 0xFFFFFFFFu, shi = 0, msp = 0, mrun = 0, gap = 0;
-    for (int64_t i = c0; i < c1; ++i) {  // the kernel's per-thread values, reduced (bc_rc.hip)
-        const uint32_t* q = rec + 4 * i;
-        const bc::RunTable T = bc::unpack_runs(q[0], q[1], q[2], q[3]);
-        const uint32_t pos = (uint32_t)h.pos[i], msn = h.seq_nib[i];
-        const uint32_t span = T.complex ? bc::full_span(h.cigar + h.cig_beg[i], h.cig_n[i]) : T.span;
-        p0 = std::min(p0, pos);
-        p1 = std::max(p1, pos + span);
-        if (T.complex) continue;
-        if (T.qlen) {
-            slo = std::min(slo, msn >> 1);
-            shi = std::max(shi, (msn + T.qlen + 1) >> 1);
-        }
-        msp = std::max(msp, T.span);
-        mrun = std::max(mrun, bc::run_shape(T));
-        gap |= T.gap ? 1u : 0u;
-    }
-    const uint32_t v[8] = {p0, p1, slo, shi, msp, mrun, gap, 0u};
-    std::memcpy(s, v, sizeof v);
-}
-std::vector<uint32_t> read_runs(const bc_reads& h, int sorted, int32_t* chunks) {
-    std::vector<uint32_t> out;
-    *chunks = 0;
-    const int64_t n = h.n_reads;
-    if (!sorted || n <= 0) return out;
-    const int64_t nch = (n + bc::kRcChunkReads - 1) / bc::kRcChunkReads;
-    const bool sums = nch < (int64_t)0x7FFFFFFF;
-    out.resize((size_t)n * 4 + (sums ? (size_t)nch * 8 : 0));
-    auto work = [&](int64_t i0, int64_t i1) {
-        for (int64_t i = i0; i < i1; ++i) {
-            const uint32_t cn = h.cig_n[i];
-            const int c = (int)(cn < (uint32_t)bc::kPre ? cn : (uint32_t)bc::kPre);
-            uint32_t w[bc::kPre] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int k = 0; k < c; ++k) w[k] = h.cigar[h.cig_beg[i] + k];
-            bc::pack_runs(bc::decode_runs<2>(w, cn, c), &out[(size_t)i * 4]);
-        }
-    };
-    auto sum = [&](int64_t k0, int64_t k1) {
-        for (int64_t k = k0; k < k1; ++k)
-            chunk_summary(h, out.data(), k * bc::kRcChunkReads, std::min<int64_t>(n, (k + 1) * bc::kRcChunkReads),
-                          &out[(size_t)n * 4 + (size_t)k * 8]);
-    };
-    const unsigned hw = std::thread::hardware_concurrency();
-    const int64_t nt = std::min<int64_t>({(int64_t)(hw ? hw : 1), 16, (n + 65535) / 65536});
-    if (nt <= 1) {
-        work(0, n);
-        if (sums) sum(0, nch);
-    } else {
-        std::vector<std::thread> th;
-        for (int64_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
-        for (auto& x : th) x.join();
-        th.clear();
-        if (sums) {
-            for (int64_t t = 0; t < nt; ++t) th.emplace_back(sum, nch * t / nt, nch * (t + 1) / nt);
-            for (auto& x : th) x.join();
-        }
-    }
-    if (sums) *chunks = (int32_t)nch;
-    return out;
+// BC_INDEX_AUTO resolved for this context: the run records when the read-chunked kernel would
+// take the batch, else the tile index when the tiled one would (the sparse sweep uses neither)
+int index_what(const bc_ctx* c, const bc_reads& r, int64_t L, int what = BC_INDEX_AUTO) {
+    if (!(what & BC_INDEX_AUTO)) return what & (BC_INDEX_RUNS | BC_INDEX_TILES);
+    if (!r.sorted || r.n_reads <= 0 || r.seq_layout != BC_SEQ_EVENT) return 0;
+    if (bc::use_rc(r, L, c->shape)) return BC_INDEX_RUNS;
+    return bc::pileup_is_solo(r, L, c->shape, c->tile_waves) ? 0 : BC_INDEX_TILES;
 }
 
 int check_host_reads(const bc_reads* r) {
@@ -412,21 +329,19 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     // conversion pass; BC_SEQ_BAM is converted in place by k_seq_event after the copy
     const bool host_event = h->seq_layout == BC_SEQ_EVENT;
     const size_t n = (size_t)h->n_reads;
-    // the tile index of a dense sorted batch (bc_reads.tile_reads): the read range of every
-    // 64-position tile, so the tiled kernel starts each tile with one load instead of a search
-    std::vector<int32_t> tidx = tile_index(*h, d->sorted, d->max_span, d->max_end);
-    // the run records of a sorted batch (bc_reads.read_runs): its CIGARs decoded once, here
-    int32_t run_chunks = 0;
-    std::vector<uint32_t> runs = read_runs(*h, d->sorted, &run_chunks);
-    constexpr int kArr = 9;
-    void* p[kArr] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // the batch's device index (bc_index.hip), built on the device after the copies: run
+    // records + chunk summaries when the read-chunked kernel would take the batch, else the tile
+    // index when the tiled one would (nothing for the sparse sweep)
+    d->seq_layout = BC_SEQ_EVENT;  // (the device copy's layout, whatever the host's)
+    const int what = index_what(c, *d, d->max_end);
+    const bc::IndexPlan plan = bc::index_plan(*d, what);
+    constexpr int kArr = 8;
+    void* p[kArr] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // the sequence buffer is sized for BC_SEQ_EVENT (converted in place after the copy)
     const size_t sz[kArr] = {n * 4, n * 4, n * 4, n * 4, (size_t)h->n_cigar_words * 4,
-                             bc::seq_event_bytes(h->seq_bytes), h->qual ? (size_t)h->qual_bytes : 0,
-                             tidx.size() * 4, runs.size() * 4};
-    const size_t cp[kArr] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6], sz[7], sz[8]};
-    const void* src[kArr] = {h->pos,  h->cig_beg, h->cig_n,   h->seq_nib,  h->cigar,
-                             h->seq,  h->qual,    tidx.data(), runs.data()};
+                             bc::seq_event_bytes(h->seq_bytes), h->qual ? (size_t)h->qual_bytes : 0, plan.total};
+    const size_t cp[kArr] = {sz[0], sz[1], sz[2], sz[3], sz[4], (size_t)h->seq_bytes, sz[6], 0};
+    const void* src[kArr] = {h->pos, h->cig_beg, h->cig_n, h->seq_nib, h->cigar, h->seq, h->qual, nullptr};
     // ONE slab for the whole batch (arrays 4 KiB-aligned inside it, the slab a multiple of 2 MiB):
     // the kernels' first touches of a batch then miss the GPU TLB on a few large fragments
     // instead of on every small buffer's pages.  The first array present is the slab base
@@ -462,12 +377,45 @@ int bc_reads_upload(bc_ctx* c, const bc_reads* h, bc_reads* d) {
     d->cigar = (const uint32_t*)p[4];
     d->seq = (const uint8_t*)p[5];
     d->qual = (const uint8_t*)p[6];
-    d->tile_reads = (const int32_t*)p[7];
-    d->n_tiles = (int64_t)tidx.size() / 2;
-    d->read_runs = (const uint32_t*)p[8];
-    d->run_chunks = run_chunks;
     d->seq_layout = BC_SEQ_EVENT;
-    HIP_TRY(hipStreamSynchronize(c->stream));  // also keeps tidx / runs alive until their copies are done
+    if (plan.total) {
+        Timed tm(c, BC_K_INDEX);
+        hipError_t e = bc::launch_index(c->stream, *d, plan, p[7]);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipFree(slab);
+            std::memset(d, 0, sizeof *d);
+            return hip_fail(e, "bc_reads_upload: index");
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BC_OK;
+}
+
+int bc_reads_index_bytes(bc_ctx* c, const bc_reads* r, int64_t L, int what, size_t* bytes) {
+    if (!c || !r || !bytes) return fail(BC_E_ARG, "NULL argument");
+    if (what & ~(BC_INDEX_RUNS | BC_INDEX_TILES | BC_INDEX_AUTO)) return fail(BC_E_ARG, "unknown BC_INDEX_* bits");
+    *bytes = bc::index_plan(*r, index_what(c, *r, L, what)).total;
+    return BC_OK;
+}
+
+int bc_reads_index(bc_ctx* c, bc_reads* r, int64_t L, int what, void* d_mem, size_t bytes) {
+    if (!c || !r) return fail(BC_E_ARG, "NULL argument");
+    if (what & ~(BC_INDEX_RUNS | BC_INDEX_TILES | BC_INDEX_AUTO)) return fail(BC_E_ARG, "unknown BC_INDEX_* bits");
+    r->read_runs = nullptr;
+    r->run_chunks = 0;
+    r->tile_reads = nullptr;
+    r->n_tiles = 0;
+    r->index_tag = 0;
+    const bc::IndexPlan plan = bc::index_plan(*r, index_what(c, *r, L, what));
+    if (!plan.total) return BC_OK;
+    if (!d_mem || bytes < plan.total) return fail(BC_E_ARG, "bc_reads_index: d_mem smaller than bc_reads_index_bytes");
+    if ((uintptr_t)d_mem & 15u) return fail(BC_E_ARG, "bc_reads_index: d_mem must be 16-byte aligned");
+    if (!r->pos || !r->cig_beg || !r->cig_n || !r->seq_nib || (r->n_cigar_words > 0 && !r->cigar))
+        return fail(BC_E_ARG, "bc_reads_index: missing per-read array");
+    DeviceGuard g(c->device);
+    Timed tm(c, BC_K_INDEX);
+    HIP_TRY(bc::launch_index(c->stream, *r, plan, d_mem));
     return BC_OK;
 }
 
@@ -475,7 +423,7 @@ int bc_reads_free(bc_ctx* c, bc_reads* d) {
     if (!c || !d) return fail(BC_E_ARG, "NULL argument");
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
-    const void* p[9] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual, d->tile_reads, d->read_runs};
+    const void* p[9] = {d->pos, d->cig_beg, d->cig_n, d->seq_nib, d->cigar, d->seq, d->qual, d->read_runs, d->tile_reads};
     for (auto q : p)  // the first array present is the base of the batch's slab (bc_reads_upload)
         if (q) {
             (void)hipFree((void*)q);
@@ -501,7 +449,7 @@ int bc_count(bc_ctx* c, const bc_reads* r, int64_t ref_len, uint32_t mbq, int nc
     }
     if (r->sorted && r->max_span <= bc::kTileMaxSpan && event) {
         // sorted batch: the tiled kernel in accumulate mode (plain read-add-write per owned tile)
-        Timed tm(c, BC_K_PILEUP);
+        Timed tm(c, bc::pileup_is_solo(*r, ref_len, c->shape, c->tile_waves) ? BC_K_SOLO : BC_K_PILEUP);
         HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, ref_len, r->max_end, mbq, ncols, false, true, 0.0, 0.0,
                                         d_hist, nullptr, nullptr, nullptr, nullptr, c->d_err, c->shape,
                                         c->tile_waves));
@@ -550,7 +498,7 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
         HIP_TRY(bc::launch_stats(c->stream, c->rc_scratch, L, k, nf, nf2, d_cov, d_pc, d_ent, d_sec, d_counts));
         return BC_OK;
     }
-    Timed tm(c, BC_K_PILEUP);
+    Timed tm(c, bc::pileup_is_solo(*r, L, c->shape, c->tile_waves) ? BC_K_SOLO : BC_K_PILEUP);
     HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, d_counts, d_cov,
                                     d_pc, d_ent, d_sec, c->d_err, c->shape, c->tile_waves));
     return BC_OK;
@@ -580,7 +528,7 @@ int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, in
     DeviceGuard g(c->device);
     bc::SumParts parts = bc::summary_parts(d_work, L);
     {
-        Timed tm(c, BC_K_PILEUP);
+        Timed tm(c, bc::pileup_is_solo(*r, L, c->shape, c->tile_waves) ? BC_K_SOLO : BC_K_PILEUP);
         HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, d_counts, d_cov,
                                         d_pc, d_ent, d_sec, c->d_err, c->shape, c->tile_waves, &parts));
     }

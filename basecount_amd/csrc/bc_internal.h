@@ -86,6 +86,34 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
 constexpr double kRcMinReadsPerTile = 2048.0;
 bool use_rc(const bc_reads& r, int64_t L, int shape);
 constexpr int kTileMaxSpan = 4096;  // beyond this span the tiled kernel's look-back gets too long
+// the tiled kernels: waves per 64-position tile from the depth (1 = the sparse sweep k_pileup_solo)
+int pileup_waves(const bc_reads& r, int64_t L, int64_t max_end, int tile_waves);
+inline bool pileup_is_solo(const bc_reads& r, int64_t L, int shape, int tile_waves) {
+    return shape != BC_SHAPE_TILE_NO_SOLO && pileup_waves(r, L, r.max_end, tile_waves) == 1;
+}
+
+// ---- the device index of a sorted batch (bc_index.hip) ----
+// bc_reads.index_tag: the batch identity an index was built for (never 0)
+inline uint64_t index_tag(const bc_reads& r) {
+    uint64_t h = 0x243F6A8885A308D3ull;
+    auto mix = [&h](uint64_t v) { h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2); };
+    mix((uint64_t)r.n_reads);
+    mix((uint64_t)(uint32_t)r.sorted);
+    mix((uint64_t)(uint32_t)r.max_span);
+    mix((uint64_t)r.max_end);
+    mix((uint64_t)(uintptr_t)r.pos);
+    mix((uint64_t)(uintptr_t)r.cig_beg);
+    return h | 1u;
+}
+inline bool index_valid(const bc_reads& r) { return r.index_tag != 0 && r.index_tag == index_tag(r); }
+struct IndexPlan {
+    size_t runs_bytes = 0, sums_bytes = 0, tiles_bytes = 0, total = 0;
+    int64_t n_chunks = 0, n_tiles = 0;
+};
+// what = BC_INDEX_RUNS | BC_INDEX_TILES (AUTO resolved by the caller)
+IndexPlan index_plan(const bc_reads& r, int what);
+// builds the planned parts into mem (plan.total bytes) and sets r's index fields and tag
+hipError_t launch_index(hipStream_t s, bc_reads& r, const IndexPlan& plan, void* mem);
 size_t summary_work_bytes(int64_t L);
 hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
                           double* out, int64_t first_chunk = 0);

@@ -942,7 +942,7 @@ PileArgs make_args(const bc_reads& r, int64_t L, uint32_t mbq) {
     A.n = r.n_reads;
     A.L = L;
     A.max_span = r.max_span;
-    if (r.tile_reads && r.n_tiles > 0 && !((uintptr_t)r.tile_reads & 7u)) {
+    if (r.tile_reads && r.n_tiles > 0 && !((uintptr_t)r.tile_reads & 7u) && index_valid(r)) {
         A.trange = (const int2*)r.tile_reads;
         A.n_trange = r.n_tiles;
     }
@@ -953,6 +953,17 @@ PileArgs make_args(const bc_reads& r, int64_t L, uint32_t mbq) {
 }
 
 }  // namespace
+
+int pileup_waves(const bc_reads& r, int64_t L, int64_t max_end, int tile_waves) {
+    if (tile_waves == 1 || tile_waves == 2 || tile_waves == 4 || tile_waves == 8) return tile_waves;
+    // waves per tile from the mean number of reads a tile walks
+    // reads overlapping a tile ~ density * (span + 63); aim for ~48 reads per wave
+    const int64_t reach = max_end > L ? max_end : L;
+    const double per_tile = reach > 0 ? (double)r.n_reads * (double)(r.max_span + kTile - 1) / (double)reach : 0.0;
+    int S = 1;
+    while (S < 8 && per_tile > 48.0 * S) S *= 2;
+    return S;
+}
 
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
@@ -974,12 +985,7 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
 #ifdef BC_DIAG
     if (const char* ab = std::getenv("BC_ABLATE")) A.ablate = std::atoi(ab);
 #endif
-    // waves per tile from the mean number of reads a tile walks
-    // reads overlapping a tile ~ density * (span + 63); aim for ~48 reads per wave
-    const double per_tile = reach > 0 ? (double)r.n_reads * (double)(r.max_span + kTile - 1) / (double)reach : 0.0;
-    int S = 1;
-    while (S < 8 && per_tile > 48.0 * S) S *= 2;
-    if (tile_waves == 1 || tile_waves == 2 || tile_waves == 4 || tile_waves == 8) S = tile_waves;
+    const int S = pileup_waves(r, L, max_end, tile_waves);
     A.S = S;
     if (parts) parts->fused = false;
     if (S == 1 && shape != BC_SHAPE_TILE_NO_SOLO) {

@@ -830,7 +830,7 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     A.mbq = mbq;
     A.seq_words = (int64_t)(seq_event_bytes(r.seq_bytes) / 4);
     A.qual_bytes = r.qual ? r.qual_bytes : 0;
-    A.runs = r.read_runs && !((uintptr_t)r.read_runs & 15u) ? (const uint4*)r.read_runs : nullptr;
+    A.runs = r.read_runs && !((uintptr_t)r.read_runs & 15u) && index_valid(r) ? (const uint4*)r.read_runs : nullptr;
     A.counts = counts;
     A.err = d_err;
     A.ablate = 0;

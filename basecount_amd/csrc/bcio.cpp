@@ -321,60 +321,46 @@ struct PhaseTimer {  // BCIO_PROFILE=1: per-phase wall times of bcio_open on std
     }
 };
 
-extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
-    if (!path || !out) return fail(BCIO_E_ARG, "null argument");
-    PhaseTimer pt;
-    nthreads = hw_threads(nthreads);
-    FileMap file;
-    int orc = file.open(path);
-    if (orc == -1) return fail(BCIO_E_IO, std::string("cannot open ") + path);
-    if (orc != 0) return fail(BCIO_E_IO, "short read");
-    const uint8_t* comp = file.data();
-    const uint64_t comp_n = file.size();
-    pt.mark("read");
-    // 1. BGZF block scan
-    std::vector<Block> blocks;
-    uint64_t off = 0, uoff = 0;
-    while (off < comp_n) {
-        if (comp_n - off < 18) return fail(BCIO_E_FORMAT, "truncated BGZF header");
-        const uint8_t* h = comp + off;
-        if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
-            return fail(BCIO_E_FORMAT, "not a BGZF file (bad gzip magic / no FEXTRA)");
-        uint16_t xlen = rd16(h + 10);
-        // the extra field itself must lie inside the file before any subfield is read
-        if ((uint64_t)12 + xlen > comp_n - off) return fail(BCIO_E_FORMAT, "truncated BGZF extra field");
-        uint64_t bsize = 0;
-        bool found = false;
-        for (uint32_t x = 0; x + 4 <= xlen;) {
-            const uint8_t* sf = h + 12 + x;
-            uint16_t slen = rd16(sf + 2);
-            if ((uint64_t)x + 4 + slen > xlen) return fail(BCIO_E_FORMAT, "BGZF subfield past the extra field");
-            if (sf[0] == 66 && sf[1] == 67 && slen == 2) {
-                bsize = (uint64_t)rd16(sf + 4) + 1;
-                found = true;
-            }
-            x += 4 + slen;
+namespace {
+
+// One BGZF block header at h[0, avail).  BCIO_OK: *b holds the deflate data's offset (from h),
+// length and inflated size, *bsize the whole block's size; 1: the block is cut off at avail (the
+// message says where); < 0: malformed.
+int scan_block(const uint8_t* h, uint64_t avail, Block* b, uint64_t* bsize_out) {
+    if (avail < 18) return (g_err = "truncated BGZF header", 1);
+    if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
+        return fail(BCIO_E_FORMAT, "not a BGZF file (bad gzip magic / no FEXTRA)");
+    uint16_t xlen = rd16(h + 10);
+    // the extra field itself must lie inside the file before any subfield is read
+    if ((uint64_t)12 + xlen > avail) return (g_err = "truncated BGZF extra field", 1);
+    uint64_t bsize = 0;
+    bool found = false;
+    for (uint32_t x = 0; x + 4 <= xlen;) {
+        const uint8_t* sf = h + 12 + x;
+        uint16_t slen = rd16(sf + 2);
+        if ((uint64_t)x + 4 + slen > xlen) return fail(BCIO_E_FORMAT, "BGZF subfield past the extra field");
+        if (sf[0] == 66 && sf[1] == 67 && slen == 2) {
+            bsize = (uint64_t)rd16(sf + 4) + 1;
+            found = true;
         }
-        if (!found) return fail(BCIO_E_FORMAT, "BGZF block without BC subfield");
-        // header (12 + xlen) + deflate data + CRC32 + ISIZE (8): a smaller BSIZE would underflow
-        // the compressed length handed to the inflater
-        if (bsize < (uint64_t)12 + xlen + 8) return fail(BCIO_E_FORMAT, "BGZF block size smaller than its header");
-        if (off + bsize > comp_n) return fail(BCIO_E_FORMAT, "truncated BGZF block");
-        Block b;
-        b.coff = off + 12 + xlen;
-        b.clen = bsize - xlen - 20;
-        b.isize = rd32(comp + off + bsize - 4);
-        if (b.isize > 65536) return fail(BCIO_E_FORMAT, "BGZF block inflates past 64 KiB");
-        b.uoff = uoff;
-        uoff += b.isize;
-        blocks.push_back(b);
-        off += bsize;
+        x += 4 + slen;
     }
-    pt.mark("scan");
-    // 2. parallel inflate
-    MapBuf raw(uoff);
-    if (!raw.ok()) return fail(BCIO_E_IO, "cannot allocate the inflate buffer");
-    pt.mark("alloc");
+    if (!found) return fail(BCIO_E_FORMAT, "BGZF block without BC subfield");
+    // header (12 + xlen) + deflate data + CRC32 + ISIZE (8): a smaller BSIZE would underflow
+    // the compressed length handed to the inflater
+    if (bsize < (uint64_t)12 + xlen + 8) return fail(BCIO_E_FORMAT, "BGZF block size smaller than its header");
+    if (bsize > avail) return (g_err = "truncated BGZF block", 1);
+    b->coff = 12 + xlen;
+    b->clen = bsize - xlen - 20;
+    b->isize = rd32(h + bsize - 4);
+    b->uoff = 0;
+    if (b->isize > 65536) return fail(BCIO_E_FORMAT, "BGZF block inflates past 64 KiB");
+    *bsize_out = bsize;
+    return BCIO_OK;
+}
+
+// Inflate every block (deflate data at comp + coff) to out + uoff, on nthreads threads.
+bool inflate_blocks(const uint8_t* comp, const std::vector<Block>& blocks, uint8_t* out, int nthreads) {
     std::atomic<int> zerr{0};
     const Deflate& ld = libdeflate();
     parallel_for((int64_t)blocks.size(), nthreads, [&](int64_t b0, int64_t b1) {
@@ -388,8 +374,7 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
                 const Block& b = blocks[i];
                 if (b.isize == 0) continue;
                 size_t got = 0;
-                if (ld.decomp(d, comp + b.coff, b.clen, raw.data() + b.uoff, b.isize, &got) != 0 ||
-                    got != b.isize)
+                if (ld.decomp(d, comp + b.coff, b.clen, out + b.uoff, b.isize, &got) != 0 || got != b.isize)
                     zerr = 1;
             }
             ld.free(d);
@@ -407,67 +392,87 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
             inflateReset(&zs);
             zs.next_in = const_cast<uint8_t*>(comp + b.coff);
             zs.avail_in = (uInt)b.clen;
-            zs.next_out = raw.data() + b.uoff;
+            zs.next_out = out + b.uoff;
             zs.avail_out = b.isize;
             int r = inflate(&zs, Z_FINISH);
             if (r != Z_STREAM_END || zs.avail_out != 0) zerr = 1;
         }
         inflateEnd(&zs);
     });
-    if (zerr) return fail(BCIO_E_ZLIB, "inflate failed");
-    pt.mark("inflate");
-    file.release();
+    return zerr == 0;
+}
 
-    // 3. BAM header
-    auto* f = new bcio_file();
-    const uint8_t* p = raw.data();
-    const uint64_t N = raw.size();
-    auto bad = [&](const char* m) {
-        delete f;
-        return fail(BCIO_E_FORMAT, m);
-    };
-    if (N < 12 || std::memcmp(p, "BAM\1", 4) != 0) return bad("missing BAM magic");
+// The BAM header (magic, text, reference list) at p[0, N): BCIO_OK and *q_end = first record
+// offset; 1 = more bytes needed (the message says what is truncated); < 0 = malformed.
+int parse_header(const uint8_t* p, uint64_t N, std::vector<std::string>& names, std::vector<int64_t>& lens,
+                 uint64_t* q_end) {
+    names.clear();
+    lens.clear();
+    if (N < 4) return (g_err = "missing BAM magic", 1);
+    if (std::memcmp(p, "BAM\1", 4) != 0) return fail(BCIO_E_FORMAT, "missing BAM magic");
+    if (N < 12) return (g_err = "missing BAM magic", 1);
     uint64_t q = 4;
     int32_t l_text = rd32s(p + q);
     q += 4;
-    if (l_text < 0 || q + (uint64_t)l_text + 4 > N) return bad("bad header text length");
+    if (l_text < 0) return fail(BCIO_E_FORMAT, "bad header text length");
+    if (q + (uint64_t)l_text + 4 > N) return (g_err = "bad header text length", 1);
     q += (uint64_t)l_text;
     int32_t n_ref = rd32s(p + q);
     q += 4;
-    if (n_ref < 0) return bad("negative n_ref");
+    if (n_ref < 0) return fail(BCIO_E_FORMAT, "negative n_ref");
     for (int32_t i = 0; i < n_ref; ++i) {
-        if (q + 4 > N) return bad("truncated reference list");
+        if (q + 4 > N) return (g_err = "truncated reference list", 1);
         int32_t ln = rd32s(p + q);
         q += 4;
-        if (ln <= 0 || q + (uint64_t)ln + 4 > N) return bad("truncated reference name");
-        f->names.emplace_back((const char*)(p + q), strnlen((const char*)(p + q), (size_t)ln));
+        if (ln <= 0) return fail(BCIO_E_FORMAT, "truncated reference name");
+        if (q + (uint64_t)ln + 4 > N) return (g_err = "truncated reference name", 1);
+        names.emplace_back((const char*)(p + q), strnlen((const char*)(p + q), (size_t)ln));
         q += (uint64_t)ln;
-        f->lens.push_back((int64_t)rd32s(p + q));
+        lens.push_back((int64_t)rd32s(p + q));
         q += 4;
     }
-    // record starts + prefix sums of cigar / seq sizes, in one hop over the record lengths.  The
-    // hop is a chain of dependent loads; prefetching the bytes each record covers, kPf ahead,
-    // turns it into a streaming read.
+    *q_end = q;
+    return BCIO_OK;
+}
+
+}  // namespace
+
+// Records from p[q0, N) into f's struct of arrays: at most max_records complete records.  With
+// partial_ok a truncated record at the end is left for a later call (*q_end = its offset);
+// without, it is a format error.  One hop over the record lengths records the starts and the
+// prefix sums of cigar / seq sizes (prefetching ahead of its load chain), then a parallel fill.
+int decode_records(bcio_file* f, const uint8_t* p, uint64_t q0, uint64_t N, int64_t max_records, bool partial_ok,
+                   int nthreads, uint64_t* q_end, PhaseTimer* pt) {
     constexpr uint64_t kPf = 4096;
+    uint64_t q = q0;
     uvec<uint64_t> starts;
-    starts.reserve(std::max<uint64_t>(16, (N - q) / 256));
+    starts.reserve(std::max<uint64_t>(16, std::min<uint64_t>((N - q) / 256, (uint64_t)std::max<int64_t>(16, max_records))));
+    f->cig_off.clear();
+    f->seq_off.clear();
     f->cig_off.reserve(starts.capacity() + 1);
     f->seq_off.reserve(starts.capacity() + 1);
     f->cig_off.push_back(0);
     f->seq_off.push_back(0);
     uint64_t cig_tot = 0, seq_tot = 0, pf = q;
-    while (q < N) {
-        if (q + 4 > N) return bad("truncated record length");
+    while (q < N && (int64_t)starts.size() < max_records) {
+        if (q + 4 > N) {
+            if (partial_ok) break;
+            return fail(BCIO_E_FORMAT, "truncated record length");
+        }
         uint32_t bs = rd32(p + q);
-        if (bs < 32 || q + 4 + bs > N) return bad("truncated BAM record");
+        if (bs < 32) return fail(BCIO_E_FORMAT, "truncated BAM record");
+        if (q + 4 + bs > N) {
+            if (partial_ok) break;
+            return fail(BCIO_E_FORMAT, "truncated BAM record");
+        }
         const uint64_t pf_end = std::min(N, q + 4 + bs + kPf);
         for (pf = std::max(pf, q + kPf); pf < pf_end; pf += 64) __builtin_prefetch(p + pf);
         const uint8_t* r = p + q + 4;
         int32_t ls = rd32s(r + 16);
-        if (ls < 0) return bad("negative l_seq");
+        if (ls < 0) return fail(BCIO_E_FORMAT, "negative l_seq");
         // the fields must fit the record before their sizes feed the output allocations
         if (32ull + r[8] + 4ull * rd16(r + 12) + (((uint64_t)ls + 1) / 2) + (uint64_t)ls > bs)
-            return bad("BAM record shorter than its fields");
+            return fail(BCIO_E_FORMAT, "BAM record shorter than its fields");
         starts.push_back(q);
         cig_tot += rd16(r + 12);
         seq_tot += (((uint64_t)ls + 1) / 2);
@@ -475,6 +480,7 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
         f->seq_off.push_back(seq_tot);
         q += 4 + (uint64_t)bs;
     }
+    *q_end = q;
     const int64_t n = (int64_t)starts.size();
     f->tid.resize(n);
     f->pos.resize(n);
@@ -490,9 +496,8 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
     f->seq_ev.resize(seq_event_bytes(seq_tot));
     std::memset(f->seq_ev.data() + seq_tot, 0, f->seq_ev.size() - seq_tot);
     f->qual.resize(2 * seq_tot);
-    pt.mark("starts");
+    if (pt) pt->mark("starts");
     std::atomic<int> ferr{0};
-    // 4b. parallel fill
     parallel_for(n, nthreads, [&](int64_t b0, int64_t b1) {
         for (int64_t i = b0; i < b1; ++i) {
             const uint8_t* r = p + starts[i] + 4;
@@ -540,8 +545,62 @@ extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
             f->rec_err[i] = err;
         }
     });
-    if (ferr) return bad("BAM record shorter than its fields");
-    pt.mark("fill");
+    if (ferr) return fail(BCIO_E_FORMAT, "BAM record shorter than its fields");
+    if (pt) pt->mark("fill");
+    return BCIO_OK;
+}
+
+extern "C" int bcio_open(const char* path, int nthreads, bcio_file** out) {
+    if (!path || !out) return fail(BCIO_E_ARG, "null argument");
+    PhaseTimer pt;
+    nthreads = hw_threads(nthreads);
+    FileMap file;
+    int orc = file.open(path);
+    if (orc == -1) return fail(BCIO_E_IO, std::string("cannot open ") + path);
+    if (orc != 0) return fail(BCIO_E_IO, "short read");
+    const uint8_t* comp = file.data();
+    const uint64_t comp_n = file.size();
+    pt.mark("read");
+    // 1. BGZF block scan
+    std::vector<Block> blocks;
+    uint64_t off = 0, uoff = 0;
+    while (off < comp_n) {
+        Block b;
+        uint64_t bsize = 0;
+        int src = scan_block(comp + off, comp_n - off, &b, &bsize);
+        if (src == 1) return fail(BCIO_E_FORMAT, g_err);
+        if (src != BCIO_OK) return src;
+        b.coff += off;
+        b.uoff = uoff;
+        uoff += b.isize;
+        blocks.push_back(b);
+        off += bsize;
+    }
+    pt.mark("scan");
+    // 2. parallel inflate
+    MapBuf raw(uoff);
+    if (!raw.ok()) return fail(BCIO_E_IO, "cannot allocate the inflate buffer");
+    pt.mark("alloc");
+    if (!inflate_blocks(comp, blocks, raw.data(), nthreads)) return fail(BCIO_E_ZLIB, "inflate failed");
+    pt.mark("inflate");
+    file.release();
+
+    // 3. BAM header, then every record
+    auto* f = new bcio_file();
+    const uint8_t* p = raw.data();
+    const uint64_t N = raw.size();
+    uint64_t q = 0;
+    int hrc = parse_header(p, N, f->names, f->lens, &q);
+    if (hrc != BCIO_OK) {
+        delete f;
+        return hrc > 0 ? fail(BCIO_E_FORMAT, g_err) : hrc;
+    }
+    uint64_t q_end = q;
+    int drc = decode_records(f, p, q, N, INT64_MAX, false, nthreads, &q_end, &pt);
+    if (drc != BCIO_OK) {
+        delete f;
+        return drc;
+    }
     raw.release();
     *out = f;
     return BCIO_OK;
@@ -691,6 +750,163 @@ extern "C" int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_se
         return fail(BCIO_E_ARG, "file too large for 32-bit batch offsets; split it");
     return BCIO_OK;
 }
+
+// ------------------------------------------------------------------------------------------
+// streaming decode (bounded memory): the file is read with pread in compressed slabs, the slab's
+// complete BGZF blocks are inflated in parallel onto the pending bytes, and each call hands out
+// the next max_records complete records as their own bcio_file.  Live memory: one batch, one
+// compressed slab and the inflated bytes not yet handed out (< one slab's worth beyond the batch).
+struct bcio_stream {
+    int fd = -1;
+    uint64_t fsize = 0, coff = 0;  // next compressed byte to read
+    int nthreads = 1;
+    std::vector<std::string> names;
+    std::vector<int64_t> lens;
+    std::vector<uint8_t> cbuf;  // compressed bytes read but not inflated (a block's start first)
+    uvec<uint8_t> pend;         // inflated bytes; [pbeg, pend.size()) not handed out yet
+    uint64_t pbeg = 0;
+    int64_t returned = 0;
+    ~bcio_stream() {
+        if (fd >= 0) ::close(fd);
+    }
+    bool all_read() const { return coff >= fsize && cbuf.empty(); }
+};
+
+namespace {
+
+constexpr uint64_t kSlab = 16ull << 20;  // compressed bytes per read
+
+// read the next compressed slab and inflate its complete blocks onto pend; BCIO_OK, or an error
+// (a block cut off by the end of the file is the whole-file decoder's truncation error)
+int stream_fill(bcio_stream* s) {
+    if (s->coff < s->fsize) {
+        const uint64_t want = std::min<uint64_t>(kSlab, s->fsize - s->coff);
+        const size_t old = s->cbuf.size();
+        s->cbuf.resize(old + want);
+        uint64_t got = 0;
+        while (got < want) {
+            ssize_t r = ::pread(s->fd, s->cbuf.data() + old + got, want - got, (off_t)(s->coff + got));
+            if (r <= 0) return fail(BCIO_E_IO, "short read");
+            got += (uint64_t)r;
+        }
+        s->coff += want;
+    }
+    std::vector<Block> blocks;
+    uint64_t off = 0, uoff = 0;
+    const uint64_t n = s->cbuf.size();
+    while (off < n) {
+        Block b;
+        uint64_t bsize = 0;
+        int rc = scan_block(s->cbuf.data() + off, n - off, &b, &bsize);
+        if (rc == 1) {
+            if (s->coff >= s->fsize) return fail(BCIO_E_FORMAT, g_err);  // nothing more will come
+            break;
+        }
+        if (rc != BCIO_OK) return rc;
+        b.coff += off;
+        b.uoff = uoff;
+        uoff += b.isize;
+        blocks.push_back(b);
+        off += bsize;
+    }
+    // drop what was handed out before growing
+    if (s->pbeg > 0) {
+        const uint64_t keep = s->pend.size() - s->pbeg;
+        std::memmove(s->pend.data(), s->pend.data() + s->pbeg, keep);
+        s->pend.resize(keep);
+        s->pbeg = 0;
+    }
+    const uint64_t base = s->pend.size();
+    s->pend.resize(base + uoff);
+    if (!inflate_blocks(s->cbuf.data(), blocks, s->pend.data() + base, s->nthreads))
+        return fail(BCIO_E_ZLIB, "inflate failed");
+    s->cbuf.erase(s->cbuf.begin(), s->cbuf.begin() + (std::ptrdiff_t)off);
+    return BCIO_OK;
+}
+
+}  // namespace
+
+extern "C" int bcio_stream_open(const char* path, int nthreads, bcio_stream** out) {
+    if (!path || !out) return fail(BCIO_E_ARG, "null argument");
+    *out = nullptr;
+    int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return fail(BCIO_E_IO, std::string("cannot open ") + path);
+    auto s = std::make_unique<bcio_stream>();
+    s->fd = fd;
+    struct stat st;
+    if (fstat(fd, &st) != 0) return fail(BCIO_E_IO, std::string("cannot stat ") + path);
+    s->fsize = (uint64_t)st.st_size;
+    s->nthreads = hw_threads(nthreads);
+    for (;;) {  // the header, however many slabs it takes
+        uint64_t q = 0;
+        int rc = parse_header(s->pend.data(), s->pend.size(), s->names, s->lens, &q);
+        if (rc == BCIO_OK) {
+            s->pbeg = q;
+            break;
+        }
+        if (rc < 0) return rc;
+        if (s->all_read()) return fail(BCIO_E_FORMAT, g_err);
+        if ((rc = stream_fill(s.get())) != BCIO_OK) return rc;
+    }
+    *out = s.release();
+    return BCIO_OK;
+}
+
+extern "C" int bcio_stream_next(bcio_stream* s, int64_t max_records, bcio_file** out) {
+    if (!s || !out || max_records <= 0) return fail(BCIO_E_ARG, "bad argument");
+    *out = nullptr;
+    // enough inflated bytes for max_records complete records, or the end of the file
+    uint64_t q_end = s->pbeg;
+    for (;;) {
+        // count complete records without decoding (the hop of decode_records, no outputs)
+        int64_t m = 0;
+        uint64_t q = s->pbeg;
+        const uint64_t N = s->pend.size();
+        const uint8_t* p = s->pend.data();
+        while (q + 4 <= N && m < max_records) {
+            const uint32_t bs = rd32(p + q);
+            if (bs < 32) return fail(BCIO_E_FORMAT, "truncated BAM record");
+            if (q + 4 + bs > N) break;
+            q += 4 + (uint64_t)bs;
+            ++m;
+        }
+        if (m >= max_records || s->all_read()) {
+            q_end = q;
+            break;
+        }
+        int rc = stream_fill(s);
+        if (rc != BCIO_OK) return rc;
+    }
+    if (q_end == s->pbeg) {
+        if (s->pbeg < s->pend.size()) {  // bytes left that never make a whole record
+            return fail(BCIO_E_FORMAT, s->pend.size() - s->pbeg < 4 ? "truncated record length" : "truncated BAM record");
+        }
+        return BCIO_OK;  // end of file
+    }
+    auto* f = new bcio_file();
+    f->names = s->names;
+    f->lens = s->lens;
+    uint64_t q_dec = s->pbeg;
+    int rc = decode_records(f, s->pend.data(), s->pbeg, q_end, max_records, false, s->nthreads, &q_dec, nullptr);
+    if (rc != BCIO_OK) {
+        delete f;
+        return rc;
+    }
+    s->pbeg = q_dec;
+    s->returned += (int64_t)f->tid.size();
+    *out = f;
+    return BCIO_OK;
+}
+
+extern "C" int64_t bcio_stream_records(const bcio_stream* s) { return s ? s->returned : -1; }
+extern "C" int32_t bcio_stream_n_refs(const bcio_stream* s) { return s ? (int32_t)s->names.size() : 0; }
+extern "C" const char* bcio_stream_ref_name(const bcio_stream* s, int32_t i) {
+    return (s && i >= 0 && i < (int32_t)s->names.size()) ? s->names[i].c_str() : nullptr;
+}
+extern "C" int64_t bcio_stream_ref_len(const bcio_stream* s, int32_t i) {
+    return (s && i >= 0 && i < (int32_t)s->lens.size()) ? s->lens[i] : -1;
+}
+extern "C" void bcio_stream_close(bcio_stream* s) { delete s; }
 
 // ------------------------------------------------------------------------------------------
 // writer

@@ -18,7 +18,8 @@ BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV, BC_E_COMM = -1, -2, -3, -4, -5
 COMM_ID_BYTES = 128  # BC_COMM_ID_BYTES
 BC_SEQ_BAM, BC_SEQ_EVENT = 0, 1
 SHAPES = {"auto": 0, "tile": 1, "rc": 2, "tile_no_solo": 3}  # BC_SHAPE_*
-KERNEL_NAMES = ("count", "stats", "rc", "pileup", "summary", "amplicons")  # BC_K_* ids
+KERNEL_NAMES = ("count", "stats", "rc", "pileup", "summary", "amplicons", "index", "solo")  # BC_K_* ids
+BC_INDEX_RUNS, BC_INDEX_TILES, BC_INDEX_AUTO = 1, 2, 4
 KERNEL_IDS = len(KERNEL_NAMES)
 
 
@@ -43,6 +44,7 @@ class BcReads(C.Structure):
         ("tile_reads", C.c_void_p),  # optional per-tile read ranges (bc_reads_upload)
         ("n_tiles", C.c_int64),
         ("read_runs", C.c_void_p),  # optional run records, 4 words per read (bc_reads_upload)
+        ("index_tag", C.c_uint64),  # the batch the index was built for (0: none)
     ]
 
 
@@ -75,6 +77,8 @@ def lib() -> C.CDLL:
         "bc_memset": ([vp, vp, C.c_int, C.c_size_t], C.c_int),
         "bc_reads_upload": ([vp, C.POINTER(BcReads), C.POINTER(BcReads)], C.c_int),
         "bc_reads_free": ([vp, C.POINTER(BcReads)], C.c_int),
+        "bc_reads_index_bytes": ([vp, C.POINTER(BcReads), i64, C.c_int, C.POINTER(C.c_size_t)], C.c_int),
+        "bc_reads_index": ([vp, C.POINTER(BcReads), i64, C.c_int, vp, C.c_size_t], C.c_int),
         "bc_count": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, vp], C.c_int),
         "bc_range_error": ([vp, C.POINTER(i64)], C.c_int),
         "bc_stats": ([vp, vp, i64, C.c_int, dbl, dbl, vp, vp, vp, vp], C.c_int),
@@ -266,6 +270,19 @@ class Context:
     def count(self, reads, ref_len: int, mbq: int, ncols: int, d_hist: int) -> None:
         r = reads.r if isinstance(reads, DeviceReads) else reads
         check(lib().bc_count(self.h, C.byref(r), int(ref_len), int(mbq), int(ncols), d_hist))
+
+    def index_bytes(self, reads, L: int, what: int = BC_INDEX_AUTO) -> int:
+        """bc_reads_index_bytes: device bytes the batch's index needs (0: nothing to build)."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        n = C.c_size_t(0)
+        check(lib().bc_reads_index_bytes(self.h, C.byref(r), int(L), int(what), C.byref(n)))
+        return int(n.value)
+
+    def index(self, reads, L: int, d_mem, nbytes: int, what: int = BC_INDEX_AUTO) -> None:
+        """bc_reads_index: build the batch's device index (run records / chunk summaries / tile
+        index) into d_mem on the stream and set the index fields of the bc_reads in place."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        check(lib().bc_reads_index(self.h, C.byref(r), int(L), int(what), d_mem, int(nbytes)))
 
     def pileup(self, reads, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec):
         """Fused kernel 1 + kernel 2 (bc_pileup) for a coordinate-sorted batch: one launch."""

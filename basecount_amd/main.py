@@ -454,7 +454,7 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
                     t = ref_index[ref]
                     L = int(reference_lengths[ref])
                     results[ref], range_idx[ref] = _device_reference(
-                        ctx, fod.reads(t), L, mbq, ncols, k, nf, nf2, _mode,
+                        ctx, _indexed(ctx, fod.reads(t), L, scratch), L, mbq, ncols, k, nf, nf2, _mode,
                         _tiles(ref) if _tiles else None, _tiles is not None, scratch)
             finally:
                 ctx.sync()
@@ -481,6 +481,16 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
         return out
     finally:
         samfile.close()
+
+
+def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
+    """The device index the kernels would use for this slice (bc_reads_index, BC_INDEX_AUTO:
+    run records + chunk summaries for the read-chunked kernel, the tile index for the tiled
+    one), built on the device into the reusable scratch, stream-ordered before the kernels."""
+    nb = ctx.index_bytes(reads, L)
+    if nb:
+        ctx.index(reads, L, scratch.get("index", nb).ptr, nb)
+    return reads
 
 
 def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_tiles=False, scratch=None):

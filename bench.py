@@ -52,8 +52,11 @@ WORKLOADS = {
     "c5": "C5: 24 contigs with GRCh38 chr1-22,X,Y lengths (3.09 Gb), 50,000 reads x 150 bp each, "
           "all-M CIGAR; contigs sharded over the ranks, summary + RCCL gather to rank 0 per step",
 }
-KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "rc": "k_rc (read-chunked kernel 1)",
+KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "solo": "k_pileup_solo (sparse sweep, fused kernel 1 + 2)",
+                "rc": "k_rc (read-chunked kernel 1)",
+                "rc_no_index": "k_rc without the device index (CIGAR words decoded in the kernel)",
                 "stats": "k_stats (kernel 2)",
+                "index": "k_index_runs + k_index_tiles (the batch's device index, bc_reads_index)",
                 "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)"}
 
 
@@ -72,7 +75,17 @@ def kernel_bytes(kernel: str, rb: int, L: int, k: int, with_pc: bool = True) -> 
     entropies; k_rc reads the batch and writes the counts; k_stats reads the counts and writes
     the statistics."""
     stats_out = L * (4 + (8 * k if with_pc else 0) + 16)
-    return {"pileup": rb + 4 * k * L + stats_out, "rc": rb + 4 * k * L, "stats": 4 * k * L + stats_out}[kernel]
+    return {"pileup": rb + 4 * k * L + stats_out, "solo": rb + 4 * k * L + stats_out, "rc": rb + 4 * k * L,
+            "rc_no_index": rb + 4 * k * L, "stats": 4 * k * L + stats_out}[kernel]
+
+
+def lib_sha16() -> str:
+    """Identity of the kernels being measured: the first 16 hex digits of the built library's
+    sha256 (profiles/kernel1_pmc.json entries carry the one their counters were read from)."""
+    import hashlib
+
+    with open(os.path.join(REPO, "basecount_amd", "libbasecount_hip.so"), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
 def host_info() -> dict:
@@ -147,17 +160,18 @@ def cpu_baseline_all_cores(b, L: int, budget_s: float = 5.0) -> dict:
                       f"per run, BAM decode excluded"}
 
 
-def e2e_c2(rs) -> dict:
-    """The CLI end to end on the C2 BAM: host decode (BGZF inflate + records,
-    including the BC_SEQ_EVENT layout), upload, kernels, download and the byte-exact TSV
-    formatter, best of 3 warm runs, output to /dev/null."""
+def e2e(cfg: str, summarise: bool = False) -> dict:
+    """The CLI end to end on the config's BAM: host decode (BGZF inflate + records,
+    including the BC_SEQ_EVENT layout), upload, the device index, kernels, download and the
+    byte-exact TSV formatter (or the summary), best of 3 warm runs, output to /dev/null."""
     from basecount_amd import fmt
     from basecount_amd import main as M
     from basecount_amd import synth
     from basecount_amd.bam import BamFile
 
+    rs = synth.make_config(cfg)
     tmp = tempfile.mkdtemp(prefix="bc_bench_")
-    bam = os.path.join(tmp, "c2.bam")
+    bam = os.path.join(tmp, f"{cfg}.bam")
     synth.write_bam(rs, bam)
 
     def best(fn, reps=3):
@@ -173,18 +187,23 @@ def e2e_c2(rs) -> dict:
             f.select(0, [True] * len(f.references))
 
     def pipeline():
-        data = M.get_basecounts(bam)
-        for ref, v in data.items():
-            d = v["rows"].d
-            fmt.rows_text(ref, d.counts, d.pc, d.ent, d.sec, 3, False)
+        data = M.get_basecounts(bam, _mode="summary" if summarise else "rows")
+        if not summarise:
+            for ref, v in data.items():
+                d = v["rows"].d
+                fmt.rows_text(ref, d.counts, d.pc, d.ent, d.sec, 3, False)
+
+    argv = [bam] + (["--summarise"] if summarise else [])
 
     def cli():
         with open(os.devnull, "w") as fh, contextlib.redirect_stdout(fh):
-            M.run([bam])
+            M.run(argv)
 
-    out = {"bam_bytes": os.path.getsize(bam), "decode_ms": best(decode),
-           "decode_count_format_ms": best(pipeline), "cli_ms": best(cli)}
-    out["cli_positions_per_s"] = rs.lengths[0] / (out["cli_ms"] * 1e-3)
+    positions = int(sum(rs.lengths))
+    out = {"config": cfg, "mode": "--summarise" if summarise else "rows", "bam_bytes": os.path.getsize(bam),
+           "reads": int(rs.n), "positions": positions, "decode_ms": best(decode),
+           "decode_count_" + ("summarise" if summarise else "format") + "_ms": best(pipeline), "cli_ms": best(cli)}
+    out["cli_positions_per_s"] = positions / (out["cli_ms"] * 1e-3)
     with contextlib.suppress(OSError):
         os.remove(bam)
         os.rmdir(tmp)
@@ -192,11 +211,15 @@ def e2e_c2(rs) -> dict:
 
 
 class Workload:
-    """One config's contigs for this rank, resident in HBM before anything is timed."""
+    """One config's contigs for this rank, resident in HBM before anything is timed.
+
+    ``copies`` > 1 uploads the same batch that many times at distinct addresses and rotates the
+    steps over them, so a batch larger than a third of the 256 MB Infinity Cache (C3: 110 MB)
+    is read from HBM on every step instead of from the cache."""
 
     def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool,
                  fused_summary: bool = True, tile_index: bool = True, streams: int = 1,
-                 read_runs: bool = True):
+                 read_runs: bool = True, copies: int = 1):
         from basecount_amd import device as D
         from basecount_amd import synth
         from basecount_amd.bam import seq_to_event
@@ -223,10 +246,14 @@ class Workload:
         self.summarise = summarise
         self.fused_summary = fused_summary
         self.nf, self.nf2 = norm_factors(self.k)
+        self.copies = max(1, int(copies))
+        self.turn = 0  # the copy the next step reads
         self.work = []
-        # host side of bc_reads_upload (its run records and tile index, built once per batch)
-        # + the copies, untimed: reported as upload_ms
+        # bc_reads_upload: host checks + H2D copies + the device index build (run records /
+        # chunk summaries / tile index, bc_index.hip), untimed: reported as upload_ms, the
+        # index's own device time as index_us
         self.upload_s = 0.0
+        self.h2d_bytes = 0
         ev = None
         for t, L in enumerate(self.rs.lengths):
             b = synth.batch_arrays(self.rs, t, 0)
@@ -234,15 +261,19 @@ class Workload:
                 ev = seq_to_event(b["seq"])
             if mbq == 0:  # qualities are never read without a threshold: not uploaded
                 b = dict(b, qual=None)
-            t_up = time.perf_counter()
-            reads = D.DeviceReads(ctx, dict(b, seq_event=ev))
-            self.upload_s += time.perf_counter() - t_up
-            assert reads.r.sorted == 1
-            if not tile_index:  # A/B: the tiled kernel searches pos[] (the index stays allocated)
-                reads.r.tile_reads = None
-                reads.r.n_tiles = 0
-            if not read_runs:  # A/B: the read-chunked kernel decodes the CIGARs itself
-                reads.r.read_runs = None
+            reads = []
+            for _ in range(self.copies):
+                t_up = time.perf_counter()
+                r = D.DeviceReads(ctx, dict(b, seq_event=ev))
+                self.upload_s += time.perf_counter() - t_up
+                assert r.r.sorted == 1
+                if not tile_index:  # A/B: the tiled kernel searches pos[] (the index stays allocated)
+                    r.r.tile_reads = None
+                    r.r.n_tiles = 0
+                if not read_runs:  # A/B: the read-chunked kernel decodes the CIGARs itself
+                    r.r.read_runs = None
+                reads.append(r)
+            self.h2d_bytes += self.copies * (16 * int(b["pos"].size) + 4 * int(b["cigar"].size) + ev.size)
             k = self.k
             bufs = dict(counts=ctx.alloc(4 * k * L), cov=ctx.alloc(4 * L),
                         pc=ctx.alloc(8 * k * L) if self.want_pc else None, ent=ctx.alloc(8 * L),
@@ -262,23 +293,30 @@ class Workload:
             j = min(range(len(load)), key=load.__getitem__)
             self.on[i] = j
             load[j] += self.work[i][1]
+        self._variants = {}
+
+    def _next(self) -> int:
+        j = self.turn
+        self.turn = (self.turn + 1) % self.copies
+        return j
 
     def step(self):
         main = self.ctx
+        j = self._next()
         for side in self.ctxs[1:]:  # fork
             side.wait(main)
         for i, (_, L, _, reads, o) in enumerate(self.work):
             ctx = self.ctxs[self.on[i]]
             pc = o["pc"].ptr if o["pc"] is not None else None
             if self.summarise and self.fused_summary:  # kernels 1 + 2 and the summary's partials
-                ctx.pileup_partials(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr,
+                ctx.pileup_partials(reads[j], L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr,
                                     o["cov"].ptr, pc, o["ent"].ptr, o["sec"].ptr, o["swork"].ptr)
             elif self.summarise:  # kernels 1 + 2, then bc_summary re-reading coverage / entropy
-                ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
+                ctx.pileup(reads[j], L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
                            pc, o["ent"].ptr, o["sec"].ptr)
                 ctx.summary(o["cov"].ptr, o["ent"].ptr, L, o["swork"].ptr, self.d_sum.ptr + 32 * i)
             else:
-                ctx.pileup(reads, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
+                ctx.pileup(reads[j], L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
                            pc, o["ent"].ptr, o["sec"].ptr)
         for side in self.ctxs[1:]:  # join
             main.wait(side)
@@ -287,9 +325,49 @@ class Workload:
             ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
                              [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
 
-    def count_only(self):
-        for _, L, _, reads, o in self.work:
-            self.ctx.count(reads, L, self.mbq, self.k, o["counts"].ptr)
+    def variant(self, name: str):
+        """Per copy and contig, a bc_reads of the same device batch: "no_index" without its
+        index (the kernels decode the CIGARs / search pos[] themselves), "rebuilt" whose index
+        is rebuilt into separate memory by rebuild() (the raw-input step)."""
+        if name not in self._variants:
+            D = self.D
+            out = []
+            for _, L, _, reads, _ in self.work:
+                per = []
+                for r in reads:
+                    s = D.BcReads.from_buffer_copy(r.r)
+                    s.read_runs, s.run_chunks, s.tile_reads, s.n_tiles, s.index_tag = None, 0, None, 0, 0
+                    mem = None
+                    if name == "rebuilt":
+                        nb = self.ctx.index_bytes(s, L)
+                        mem = (self.ctx.alloc(nb), nb) if nb else None
+                    per.append((s, mem))
+                out.append(per)
+            self._variants[name] = out
+        return self._variants[name]
+
+    def rebuild(self):
+        """The device index of the next copy's batch, built again (bc_reads_index)."""
+        j = self._next()
+        for (_, L, _, _, _), per in zip(self.work, self.variant("rebuilt")):
+            s, mem = per[j]
+            if mem is not None:
+                self.ctx.index(s, L, mem[0].ptr, mem[1])
+        self.turn = j  # the matching step reads the same copy
+
+    def raw_step(self):
+        """One step from the raw batch: index build + the step's kernels on that copy."""
+        self.rebuild()
+        j = self._next()
+        for (_, L, _, _, o), per in zip(self.work, self.variant("rebuilt")):
+            self.ctx.pileup(per[j][0], L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
+                            o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
+
+    def count_only(self, variant: str | None = None):
+        j = self._next()
+        for i, (_, L, _, reads, o) in enumerate(self.work):
+            r = reads[j] if variant is None else self.variant(variant)[i][j][0]
+            self.ctx.count(r, L, self.mbq, self.k, o["counts"].ptr)
 
     def stats_only(self):
         for _, L, _, _, o in self.work:
@@ -337,8 +415,15 @@ class Workload:
         return synth.ref_events(self.rs)
 
     def free(self):
+        for per_contig in self._variants.values():
+            for per in per_contig:
+                for _, mem in per:
+                    if mem is not None:
+                        mem[0].free()
+        self._variants = {}
         for _, _, _, reads, o in self.work:
-            reads.free()
+            for r in reads:
+                r.free()
             for v in o.values():
                 if v is not None:
                     v.free()
@@ -369,8 +454,9 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     max over ranks) and describe them."""
     from basecount_amd import device as D
 
+    copies = args.rotate if args.rotate > 0 else (3 if cfg == "c3" else 1)
     wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused",
-                  args.tile_index == "on", args.streams if summarise else 1, args.read_runs == "on")
+                  args.tile_index == "on", args.streams if summarise else 1, args.read_runs == "on", copies)
     rccl = group is not None and getattr(group, "backend", "") == "rccl"
     gather = None
     if summarise and group is not None:
@@ -447,20 +533,23 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
             for name, (n_launch, mean_us) in c.timing_report().items():
                 rep[name] = rep.get(name, 0.0) + n_launch * mean_us
             c.timing(False)
-        for name in ("pileup", "rc", "stats", "summary"):
+        for name in ("pileup", "solo", "rc", "stats", "summary"):
             if name in rep:
                 kern_s[name] = rep[name] * 1e-6 / reps_t
-    elif "pileup" in launched:
-        def pile_only():
-            for _, L, _, reads, o in wl.work:
-                ctx.pileup(reads, L, wl.mbq, wl.k, wl.nf, wl.nf2, o["counts"].ptr, o["cov"].ptr,
-                           o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
+    elif "pileup" in launched or "solo" in launched:
         # eager back-to-back launches: the kernel's own average duration (what rocprofv3's kernel
         # trace reports); a graph replay hides part of the launch gap and would flatter it
-        kern_s["pileup"] = region(pile_only, reps)
+        kern_s["pileup" if "pileup" in launched else "solo"] = region(wl.step, reps)
+    extra_us = {}
     if "rc" in launched and not summarise:  # deep: k_rc + k_stats (bc_count: k_rc alone)
         kern_s["rc"] = region(wl.count_only, reps)
         kern_s["stats"] = region(wl.stats_only, reps)
+        # what the step does not pay for: k_rc from the raw batch (CIGAR words
+        # decoded in the kernel), the device index build on its own, and whole steps from the
+        # raw batch (index build + k_rc + k_stats)
+        kern_s["rc_no_index"] = region(lambda: wl.count_only("no_index"), reps)
+        kern_s["index"] = region(wl.rebuild, reps)
+        extra_us["raw_step_us"] = region(wl.raw_step, reps) * 1e6
     gather_us = None
     if gather is not None:
         if group is not None:
@@ -468,7 +557,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         gather_us = region(gather_step, reps) * 1e6
     wl.step()  # restore the step's outputs (count-only regions accumulated into the counts)
     ctx.sync()
-    dom = max((k for k in kern_s if k != "summary"), key=kern_s.get)
+    dom = max((k for k in kern_s if k in ("pileup", "solo", "rc")), key=kern_s.get)
 
     parity = wl.parity()
     if gather is not None and rccl:
@@ -487,12 +576,15 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     # roofline then uses the whole step's device time (fold included), a lower bound
     basis_s = dev_step if len(wl.ctxs) > 1 else kern_s[dom]
     achieved = kbytes / basis_s / 1e9
+    # HBM bytes per launch from the PMC passes (scripts/pmc.sh), only when they were read from
+    # this very library (sha) on the same workload: otherwise null, never a stale figure
     traffic = None
     pmc = os.path.join(REPO, "profiles", "kernel1_pmc.json")
     if os.path.exists(pmc) and world == 1:
         with open(pmc) as fh:
             pm = json.load(fh).get(cfg, {})
-        if pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom:
+        if (pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom
+                and pm.get("lib_sha16") == lib_sha16() and pm.get("copies", 1) == copies):
             traffic = pm.get("hbm_bytes_per_launch")
     res = {
         "workload": WORKLOADS[cfg],
@@ -506,6 +598,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         "kernel_us": {KERNEL_NAMES[n]: v * 1e6 for n, v in kern_s.items()},
         "kernels": ("k_pileup (kernel 1 and kernel 2 fused), one launch per contig per step"
                     if dom == "pileup" else
+                    "k_pileup_solo (sparse sweep, kernel 1 and kernel 2 fused), one launch per contig per step"
+                    if dom == "solo" else
                     "k_rc (kernel 1, into a zeroed scratch) + k_stats (kernel 2, moves the counts out "
                     "and re-zeroes) per contig per step")
                    + (", + numpy-exact summary per contig" if summarise else "")
@@ -517,6 +611,10 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         "contigs_per_rank": len(wl.work),
         "streams": len(wl.ctxs),
         "upload_ms": wl.upload_s * 1e3,
+        "upload": {"ms": wl.upload_s * 1e3, "h2d_bytes": wl.h2d_bytes, "copies": wl.copies,
+                   "what": "bc_reads_upload per batch copy: host argument checks + H2D + the device index "
+                           "build (index_us, when measured, is that build alone)"},
+        "batch_copies": wl.copies,
         "parity_vs_oracle": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_NAMES[dom],
@@ -524,6 +622,11 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                      else "kernel's average duration",
                      "algorithmic_bytes": kbytes},
     }
+    res.update(extra_us)
+    if "rc" in kern_s:
+        nb = wl.bytes_dominant("rc")
+        res["rc_frac_without_index"] = nb / kern_s["rc_no_index"] / 1e9 / HBM_PEAK_GBS
+        res["index_us"] = kern_s["index"] * 1e6
     if gather_us is not None:
         res["gather_us"] = gather_us
         res["gather_bytes"] = int(gather[0].sum())
@@ -621,6 +724,9 @@ def main():
                     help="c5: contexts (streams) the contigs run on concurrently (bc_ctx_wait fork/join)")
     ap.add_argument("--read-runs", choices=["on", "off"], default="on",
                     help="off: drop the upload's run records (bc_reads.read_runs), A/B only")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="device copies of each batch the steps rotate over (0: 3 for c3, whose 110 MB "
+                         "would otherwise stay in the 256 MB Infinity Cache, else 1)")
     ap.add_argument("--tile-index", choices=["on", "off"], default="on",
                     help="off: drop the upload's per-tile read ranges (bc_reads.tile_reads), A/B only")
     ap.add_argument("--allow-diag", action="store_true",
@@ -689,7 +795,7 @@ def main():
             r.pop("_wl").free()
             extra[cfg] = r
 
-    cpu = cpu_all = e2e = None
+    cpu = cpu_all = e2e_res = None
     if rank == 0 and world == 1:
         from basecount_amd import synth
 
@@ -699,7 +805,11 @@ def main():
             cpu = cpu_baseline(rs, b0, rs.lengths[0], args.cpu_budget)
             cpu_all = cpu_baseline_all_cores(b0, rs.lengths[0], min(5.0, args.cpu_budget))
         if not args.no_e2e and args.config == "c2":
-            e2e = e2e_c2(synth.make_config("c2"))
+            e2e_res = e2e("c2")
+            if not args.no_extras:  # the other shapes' CLI paths too
+                for cfg, summ in (("c3", False), ("c5", True)):
+                    if cfg in extra:
+                        extra[cfg]["e2e"] = e2e(cfg, summ)
 
     if rank == 0:
         line = {
@@ -723,7 +833,7 @@ def main():
                        "comm": (group.backend if group is not None else None),
                        "shape": args.shape, "tile_waves": args.tile_waves,
                        "summary_path": args.summary_path, "tile_index": args.tile_index,
-                       "read_runs": args.read_runs, "build": build},
+                       "read_runs": args.read_runs, "build": build, "lib_sha16": lib_sha16()},
             "gbases_piled_per_s": head["gbases_piled_per_s"],
             "device_us_per_step": head["device_us_per_step"],
             "upload_ms": head["upload_ms"],
@@ -734,7 +844,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "gather_ms": gather_ms,
-            "e2e": e2e,
+            "e2e": e2e_res,
             "extra": extra,
         }
         if "gather_us" in head:

@@ -42,7 +42,7 @@ extern "C" {
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
 #define BC_E_COMM (-5)  /* RCCL error in a multi-GPU call                                        */
 
-#define BC_ABI_VERSION 6
+#define BC_ABI_VERSION 7
 
 /* Layouts of bc_reads.seq.
  *   BC_SEQ_BAM   BAM packing: "=ACMGRSVTWYHKDBN" codes, two per byte, high nibble first
@@ -98,6 +98,12 @@ typedef struct bc_reads {
      * first / last-plus-one byte of their aligned sequence, max span, a run-shape code and a
      * deletion flag over the reads with simple CIGARs (bc_runs.h: chunk_summary).              */
     const uint32_t* read_runs;
+    /* Identity of the batch the index above was built for (bc_reads_upload / bc_reads_index):
+     * a hash of n_reads, sorted, max_span, max_end and the pos / cig_beg pointers.  The kernels
+     * use tile_reads / read_runs only while it matches, so a copied struct that was sliced (pos
+     * offset, n_reads shrunk) or given another max_span falls back to searching / decoding
+     * instead of reading another batch's index.  0 = no index.                              */
+    uint64_t index_tag;
 } bc_reads;
 
 typedef struct bc_ctx bc_ctx;
@@ -154,6 +160,23 @@ int bc_seq_to_event(bc_ctx* ctx, const uint8_t* d_bam, int64_t seq_bytes, uint8_
 int bc_reads_upload(bc_ctx* ctx, const bc_reads* h_reads, bc_reads* d_reads);
 int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
 
+/* The device index of a sorted batch assembled in device memory by the caller (e.g. one
+ * reference's slice of a file-wide upload), built ON THE DEVICE into caller-owned memory:
+ *   BC_INDEX_RUNS   run records + k_rc chunk summaries (read_runs, run_chunks)
+ *   BC_INDEX_TILES  the tile index (tile_reads, n_tiles; dense batches only)
+ *   BC_INDEX_AUTO   what this context's kernels would use for a reference of length ref_len
+ *                   (records for the read-chunked shape, tiles for the tiled one, nothing for
+ *                   the sparse sweep)
+ * bc_reads_index_bytes gives the bytes d_mem must hold (0: nothing to build); bc_reads_index
+ * launches the build on the context's stream (async, no allocation: capturable) and sets the
+ * index fields and index_tag of *d_reads.  d_reads->sorted / max_span / max_end must be
+ * truthful.  bc_reads_upload builds BC_INDEX_AUTO for ref_len = max_end into its own slab.    */
+#define BC_INDEX_RUNS 1
+#define BC_INDEX_TILES 2
+#define BC_INDEX_AUTO 4
+int bc_reads_index_bytes(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, int what, size_t* bytes);
+int bc_reads_index(bc_ctx* ctx, bc_reads* d_reads, int64_t ref_len, int what, void* d_mem, size_t bytes);
+
 /* Kernel 1 — CIGAR-expand + scatter-add (count.cpp:22-97).
  * Accumulates into d_hist, an int32 histogram of `ncols` planes of `ref_len` positions
  * (plane-major: d_hist[c * ref_len + p]).  ncols = 6 gives the reference's full layout
@@ -209,7 +232,9 @@ int bc_ctx_wait(bc_ctx* ctx, bc_ctx* other);
 #define BC_K_PILEUP 3     /* fused tiled kernel 1 + 2                              */
 #define BC_K_SUMMARY 4
 #define BC_K_AMPLICONS 5
-#define BC_KERNEL_IDS 6
+#define BC_K_INDEX 6      /* the device index build (bc_reads_index / bc_reads_upload)  */
+#define BC_K_SOLO 7       /* the sparse sweep k_pileup_solo (fused kernel 1 + 2)     */
+#define BC_KERNEL_IDS 8
 int bc_timing_enable(bc_ctx* ctx, int on);
 int bc_timing_report(bc_ctx* ctx, int64_t* launches /* [BC_KERNEL_IDS] */, double* mean_us /* [..] */);
 

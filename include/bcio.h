@@ -102,6 +102,23 @@ typedef struct bcio_selection {
 
 int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_sel, bcio_selection* out);
 
+/* ---- streaming decode: bounded memory (the reference's --chunk-size, main.py:142-162) ----------
+ * bcio_stream_open reads the header; bcio_stream_next decodes the next at most max_records records
+ * (file order) into a new bcio_file handle — bcio_get_records / bcio_select work on it as on a
+ * whole file, its record indices and ordinals counting from the batch's first record — which the
+ * caller releases with bcio_close.  *out = NULL at the end of the file.  Live memory is one
+ * batch plus a compressed slab and its inflated bytes (the file is read with pread, never
+ * mapped whole).  bcio_stream_records: records handed out so far (the next batch's first
+ * record index in the file).                                                                  */
+typedef struct bcio_stream bcio_stream;
+int bcio_stream_open(const char* path, int nthreads, bcio_stream** out);
+int bcio_stream_next(bcio_stream* s, int64_t max_records, bcio_file** out);
+int64_t bcio_stream_records(const bcio_stream* s);
+int32_t bcio_stream_n_refs(const bcio_stream* s);
+const char* bcio_stream_ref_name(const bcio_stream* s, int32_t i);
+int64_t bcio_stream_ref_len(const bcio_stream* s, int32_t i);
+void bcio_stream_close(bcio_stream* s);
+
 /* BAM-packed SEQ bytes -> BC_SEQ_EVENT (basecount_hip.h), on the host with `nthreads` threads
  * (<= 0: hardware).  out_bytes >= nbytes rounded up to 16 plus 16; the tail is zero-filled.
  * The decoder already provides this layout for a file's records (bcio_records.seq_event).   */

@@ -32,7 +32,7 @@ import numpy as np
 
 from . import device as D
 from . import fmt
-from .bam import REC_BAD_CLIP, REC_NEG_POS, REC_NO_CIGAR, REC_NO_QUAL, REC_NO_SEQ, BamFile
+from .bam import REC_BAD_CLIP, REC_NEG_POS, REC_NO_CIGAR, REC_NO_QUAL, REC_NO_SEQ, BamFile, BamStream
 from .scheme import load_scheme
 from .version import __version__
 
@@ -276,44 +276,59 @@ def _bad_pos(f: BamFile, rec: int, mbq: int, L: int) -> int:
     return -1
 
 
-def _first_error(f, sel, ref_order, ref_index, lengths, mbq, cs, type_ord, range_idx):
-    """Replay the reference's read loop / chunk-flush timeline (main.py:141-189) and return the
-    exception it raises first, or None.
+class _Faults:
+    """What the reference's read loop (main.py:141-189) would raise, gathered while the file
+    streams by: every position is a global accepted-read ordinal (file order), so the batches
+    the file is decoded in (bounded memory) need not match the reference's chunks.
 
-    type_ord[ref]  : first accepted-read ordinal of the ref with a None field / negative start
-    range_idx[ref] : first batch index whose counted event lies outside the reference
+      keyerror : (ordinal, reference name) of the first accepted read of an unrequested
+                 reference (main.py:166 indexes read_chunk by it)
+      clip     : ordinal of the first selected read whose clipping pysam rejects (main.py:167)
+      type_ord : ref -> ordinal of its first read with a None field / negative start
+      range_   : ref -> (ordinal, refPos) of its first read with a counted event >= ref_len
     """
+
+    def __init__(self):
+        self.keyerror = None
+        self.clip = None
+        self.type_ord = {}
+        self.range_ = {}
+        self.n_records = 0
+
+    def inloop(self):
+        """The first in-loop fault (ordinal, exception) or None (KeyError before ValueError on
+        the same read: the chunk is indexed before the sequence is fetched)."""
+        out = None
+        if self.keyerror is not None:
+            out = (self.keyerror[0], KeyError(self.keyerror[1]))
+        if self.clip is not None and (out is None or self.clip < out[0]):
+            out = (self.clip, ValueError("Invalid clipping in CIGAR string"))
+        return out
+
+
+def _first_error(fl: _Faults, ref_order, lengths, mbq, cs, type_args):
+    """Replay the reference's read loop / chunk-flush timeline (main.py:141-189) and return the
+    exception it raises first, or None.  ``type_args(ref, lo, hi)``: the pysam-shaped arguments
+    of the ref's accepted reads with ordinals in [lo, hi) (hi None: to the end of the file)."""
     mbq_bad = not (0 <= mbq < _U32)
-    # in-loop faults: KeyError for an unrequested reference (main.py:166), pysam's ValueError
-    # for invalid clipping when a selected read's sequence is fetched (main.py:167)
-    inloop = None
-    if sel.keyerror_ordinal >= 0:
-        t = int(f.tid[sel.keyerror_rec])
-        name = f.references[t] if 0 <= t < len(f.references) else None
-        inloop = (sel.keyerror_ordinal, KeyError(name))
-    clip = (f.rec_err[sel.rec] & REC_BAD_CLIP) != 0
-    if clip.any():
-        o = int(sel.ordinal[np.argmax(clip)])
-        if inloop is None or o < inloop[0]:
-            inloop = (o, ValueError("Invalid clipping in CIGAR string"))
+    inloop = fl.inloop()
 
     def chunk_of(o):
         return o // cs if cs > 0 else 0
 
-    faults = {}  # ref -> (chunk, kind, ordinal/idx)
+    faults = {}  # ref -> (chunk, kind)
     for ref in ref_order:
         cand = []
         if mbq_bad:
-            cand.append((0, 0, "type", None))
-        if type_ord.get(ref, -1) >= 0:
-            cand.append((chunk_of(type_ord[ref]), 0, "type", None))
-        if range_idx.get(ref, -1) >= 0:
-            t = ref_index[ref]
-            o = int(sel.ordinal[sel.ref_beg[t] + range_idx[ref]])
-            cand.append((chunk_of(o), 1, "range", range_idx[ref]))
+            cand.append((0, 0, "type"))
+        if fl.type_ord.get(ref, -1) >= 0:
+            cand.append((chunk_of(fl.type_ord[ref]), 0, "type"))
+        if ref in fl.range_:
+            cand.append((chunk_of(fl.range_[ref][0]), 1, "range"))
         if cand:
             faults[ref] = min(cand, key=lambda c: (c[0], c[1]))
-    if cs == 0 and mbq_bad and f.n_records > 0 and ref_order:
+    empty_first_flush = cs == 0 and mbq_bad and fl.n_records > 0 and bool(ref_order)
+    if empty_first_flush:
         inloop = None  # the empty flush at the first record raises before anything else
     if not faults:
         return inloop[1] if inloop else None
@@ -325,27 +340,53 @@ def _first_error(f, sel, ref_order, ref_index, lengths, mbq, cs, type_ord, range
         v = faults.get(ref)
         if v is None or v[0] != kf:
             continue
-        t = ref_index[ref]
-        b0, b1 = int(sel.ref_beg[t]), int(sel.ref_beg[t + 1])
         if v[2] == "type":
-            ords = sel.ordinal[b0:b1]
-            m = (ords // cs == kf) if cs > 0 else np.ones(b1 - b0, bool)
-            recs = sel.rec[b0:b1][m]
-            args = [lengths[ref], mbq] + list(_pysam_args(f, recs))
+            if empty_first_flush:  # bcount(L, mbq, [], [], [], []) at the first record
+                reads = ([], [], [], [])
+            elif cs > 0:
+                reads = type_args(ref, kf * cs, (kf + 1) * cs)
+            else:
+                reads = type_args(ref, 0, None)
+            args = [lengths[ref], mbq] + list(reads)
             return TypeError(_SIG + ", ".join(repr(a) for a in args))
-        rec = int(sel.rec[b0 + v[3]])
         L = lengths[ref]
-        return IndexError(f"vector::_M_range_check: __n (which is {_bad_pos(f, rec, mbq, L)}) "
+        return IndexError(f"vector::_M_range_check: __n (which is {fl.range_[ref][1]}) "
                           f">= this->size() (which is {L})")
     return None
 
 
-# ------------------------------------------------------------------------- device pipeline
-class _FileOnDevice:
-    """Shared per-file buffers in HBM: CIGAR words, packed SEQ, nibble-indexed QUAL, and the
-    per-read arrays of every selected read (sliced per reference)."""
+def _type_args(bam, batch_records_, mmq, wanted, ref_index):
+    """type_args for _first_error: a second pass over the file (error path only) collecting the
+    pysam-shaped arguments of one reference's reads in an ordinal range."""
 
-    def __init__(self, ctx: D.Context, f: BamFile, sel, need_qual: bool):
+    def collect(ref, lo, hi):
+        t = ref_index[ref]
+        out = ([], [], [], [])
+        base = 0
+        with BamStream(bam) as st:
+            for f in st.batches(batch_records_):
+                sel = f.select(mmq, wanted)
+                b0, b1 = int(sel.ref_beg[t]), int(sel.ref_beg[t + 1])
+                ords = sel.ordinal[b0:b1] + base
+                m = (ords >= lo) & ((ords < hi) if hi is not None else True)
+                for dst, src in zip(out, _pysam_args(f, sel.rec[b0:b1][m])):
+                    dst.extend(src)
+                base += sel.n_accepted
+                if hi is not None and base >= hi:
+                    break
+        return out
+
+    return collect
+
+
+# ------------------------------------------------------------------------- device pipeline
+class _BatchOnDevice:
+    """One decoded batch in HBM: CIGAR words, packed SEQ (BC_SEQ_EVENT), nibble-indexed QUAL and
+    the per-read arrays of its selected reads (sliced per reference).  The buffers come from the
+    call's grow-only scratch, so batch after batch reuses the same HBM (stream-ordered: a batch's
+    upload follows the previous batch's kernels on the one stream)."""
+
+    def __init__(self, ctx: D.Context, f: BamFile, sel, need_qual: bool, scratch):
         self.ctx = ctx
         rec_err = f.rec_err[sel.rec] if sel.rec.size else np.zeros(0, np.uint32)
         faulty = (rec_err & (_TYPE_FAULTS | REC_BAD_CLIP)) != 0
@@ -356,18 +397,18 @@ class _FileOnDevice:
         self.sel = sel
         # reference spans per read (for the LDS window bound), from the decoder
         self.span = np.where(faulty, 0, sel.span)
-        self.d_cigar = ctx.alloc(max(4, f.cigar.nbytes)).upload(f.cigar)
+        self.d_cigar = scratch.get("b_cigar", max(4, f.cigar.nbytes)).upload(f.cigar)
         # packed SEQ in the kernels' layout (BC_SEQ_EVENT, padded): the decoder built it while
         # filling the records, so the upload is a plain copy (no device conversion pass)
         assert f.seq_event.size == D.seq_event_bytes(f.seq.nbytes)
-        self.d_seq = ctx.alloc(f.seq_event.size).upload(f.seq_event)
-        self.d_qual = ctx.alloc(max(4, f.qual.nbytes)).upload(f.qual) if need_qual else None
+        self.d_seq = scratch.get("b_seq", f.seq_event.size).upload(f.seq_event)
+        self.d_qual = scratch.get("b_qual", max(4, f.qual.nbytes)).upload(f.qual) if need_qual else None
         self.n_cig, self.n_seq, self.n_qual = f.cigar.size, f.seq.size, f.qual.size
         m = sel.pos.size
-        self.d_pos = ctx.alloc(max(4, 4 * m)).upload(self.pos)
-        self.d_cb = ctx.alloc(max(4, 4 * m)).upload(sel.cig_beg)
-        self.d_cn = ctx.alloc(max(4, 4 * m)).upload(self.cig_n)
-        self.d_sn = ctx.alloc(max(4, 4 * m)).upload(sel.seq_nib)
+        self.d_pos = scratch.get("b_pos", max(4, 4 * m)).upload(self.pos)
+        self.d_cb = scratch.get("b_cb", max(4, 4 * m)).upload(sel.cig_beg)
+        self.d_cn = scratch.get("b_cn", max(4, 4 * m)).upload(self.cig_n)
+        self.d_sn = scratch.get("b_sn", max(4, 4 * m)).upload(sel.seq_nib)
 
     def reads(self, t: int) -> D.BcReads:
         b0, b1 = int(self.sel.ref_beg[t]), int(self.sel.ref_beg[t + 1])
@@ -392,6 +433,22 @@ class _FileOnDevice:
         return r
 
 
+def batch_records(chunk_size: int) -> int:
+    """Records per decoded batch: the reference's chunk size (main.py:142, accepted reads held
+    in memory at once) bounded to [2^16, 2^24] records, 2^22 when it does not bound anything
+    (chunk_size <= 0).  BASECOUNT_BATCH_RECORDS overrides (tests: many tiny batches)."""
+    v = os.environ.get("BASECOUNT_BATCH_RECORDS")
+    if v:
+        return max(1, int(v))
+    cs = int(chunk_size)
+    return min(max(cs, 1 << 16), 1 << 24) if cs > 0 else 1 << 22
+
+
+class _Ungrouped(Exception):
+    """A reference's reads came back after the reference was finished (the file is not grouped
+    by reference): start again, accumulating every reference until the end of the file."""
+
+
 def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality=0,
                    chunk_size=1000000, show_n_bases=False, long_format=False, *, device=None,
                    _mode="rows", _tiles=None, _group=None):
@@ -399,78 +456,168 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
     reference's (set) order.  ``_mode="summary"`` keeps per-position data in HBM and returns
     the numpy-exact summary (and amplicon) reductions instead of rows.
 
+    The BAM streams through in batches of records (``batch_records(chunk_size)``, the
+    reference's chunked read loop): host and HBM memory hold one batch (two while the next is
+    decoded) plus the per-reference outputs, not the file.  A reference whose reads all lie in
+    one batch takes the fused pileup (kernels 1 + 2 in one pass); one spread over several
+    batches is accumulated batch by batch (bc_count) and finished by kernel 2 after its last.
+
     With ``_group`` (a dist.Group, one process per GPU) the references are sharded over the
     ranks (dist.shard): this rank computes and returns only the ones it owns, and the function
     returns ``(results, owner, order)``; every rank raises the same first error."""
-    samfile = open_samfile(bam)
+    args = (bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
+            long_format, device, _mode, _tiles, _group)
     try:
-        references = get_references(samfile, references)
-        names = samfile.references
+        return _get_basecounts(*args, grouped=True)
+    except _Ungrouped:
+        return _get_basecounts(*args, grouped=False)
+
+
+def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
+                    long_format, device, _mode, _tiles, _group, grouped):
+    stream = BamStream(bam)
+    try:
+        references = get_references(stream, references)
+        names = stream.references
         ref_index = {n: i for i, n in enumerate(names)}
-        reference_lengths = {ref: samfile.lengths[names.index(ref)] for ref in references}
+        reference_lengths = {ref: stream.lengths[names.index(ref)] for ref in references}
         ref_order = list(references)
         if _group is not None:
             from .dist import agree_order
 
             # main.py:92's set order is per process (hash seed): every rank follows rank 0's
             ref_order = agree_order(_group, ref_order)
-        sel = samfile.select(min_mapping_quality, [n in references for n in names])
+        mmq = min_mapping_quality
+        wanted = [n in references for n in names]
         mbq = int(min_base_quality)
+        mbq_ok = 0 <= mbq < _U32
         k = 6 if show_n_bases else 5
         ncols = k  # N is only ever reported with show_n_bases
-        rec_err = samfile.rec_err[sel.rec] if sel.rec.size else np.zeros(0, np.uint32)
-        type_ord = {}
-        for ref in ref_order:
-            t = ref_index[ref]
-            b0, b1 = int(sel.ref_beg[t]), int(sel.ref_beg[t + 1])
-            m = (rec_err[b0:b1] & _TYPE_FAULTS) != 0
-            type_ord[ref] = int(sel.ordinal[b0 + int(np.argmax(m))]) if m.any() else -1
-
-        nreads = {ref: int(sel.ref_beg[ref_index[ref] + 1] - sel.ref_beg[ref_index[ref]])
-                  for ref in ref_order}
         owner = None
         mine = ref_order
         if _group is not None:
             from .dist import shard
 
-            # cost estimate: per-position outputs + per-read work (both linear)
-            owner = shard(ref_order, {r: int(reference_lengths[r]) + 100 * nreads[r] for r in ref_order},
-                          _group.world)
+            # cost estimate before any read is seen: the per-position outputs (linear in length)
+            owner = shard(ref_order, {r: int(reference_lengths[r]) for r in ref_order}, _group.world)
             mine = [r for r in ref_order if owner[r] == _group.rank]
-        results, range_idx = {}, {}
-        if 0 <= mbq < _U32 and mine:
-            ctx = context(device)
-            fod = _FileOnDevice(ctx, samfile, sel, need_qual=mbq > 0)
-            nf, nf2 = norm_factors(k)
-            scratch = _Scratch(ctx)
-            try:
-                # sized once for the longest reference
-                Lmax = max(int(reference_lengths[r]) for r in mine)
-                scratch.outputs(k, Lmax, _mode == "rows")
-                scratch.get("hist", 4 * ncols * Lmax)
-                if _mode != "rows":
-                    scratch.get("work", D.summary_work_bytes(Lmax))
-                for ref in mine:
+        mine_t = {ref_index[r] for r in mine}
+        B = batch_records(chunk_size)
+        fl = _Faults()
+        nreads = {ref: 0 for ref in ref_order}
+        results = {}
+        acc = {}  # ref -> device histogram accumulating its batches (int32 [ncols][L])
+        finished = set()
+        ctx = context(device) if (mbq_ok and mine) else None
+        scratch = _Scratch(ctx) if ctx is not None else None
+        nf, nf2 = norm_factors(k)
+
+        def tiles_of(ref):
+            return _tiles(ref) if _tiles else None
+
+        base = 0  # accepted reads before the current batch (global ordinals)
+        cur = nxt = None
+        try:
+            cur = stream.next_batch(B)
+            sel_next = None
+            while cur is not None:
+                f = cur
+                sel = sel_next if sel_next is not None else f.select(mmq, wanted)
+                sel_next = None
+                fl.n_records += f.n_records
+                # in-loop faults (global ordinals); type faults per reference
+                if fl.keyerror is None and sel.keyerror_ordinal >= 0:
+                    t = int(f.tid[sel.keyerror_rec])
+                    fl.keyerror = (base + sel.keyerror_ordinal, names[t] if 0 <= t < len(names) else None)
+                rec_err = f.rec_err[sel.rec] if sel.rec.size else np.zeros(0, np.uint32)
+                clip = (rec_err & REC_BAD_CLIP) != 0
+                if fl.clip is None and clip.any():
+                    fl.clip = base + int(sel.ordinal[np.argmax(clip)])
+                here = []
+                for ref in ref_order:
                     t = ref_index[ref]
+                    b0, b1 = int(sel.ref_beg[t]), int(sel.ref_beg[t + 1])
+                    if b1 == b0:
+                        continue
+                    nreads[ref] += b1 - b0
+                    m = (rec_err[b0:b1] & _TYPE_FAULTS) != 0
+                    if fl.type_ord.get(ref, -1) < 0 and m.any():
+                        fl.type_ord[ref] = base + int(sel.ordinal[b0 + int(np.argmax(m))])
+                    if t in mine_t:
+                        here.append(ref)
+                # one batch of look-ahead: a reference absent from the next batch is complete
+                # (in a file grouped by reference); none after the reference's first in-loop fault
+                nxt = stream.next_batch(B) if fl.inloop() is None else None
+                if ctx is not None and here:
+                    if any(r in finished for r in here):
+                        raise _Ungrouped()
+                    nsel = sel_next = nxt.select(mmq, wanted) if (nxt is not None and grouped) else None
+                    bod = _BatchOnDevice(ctx, f, sel, need_qual=mbq > 0, scratch=scratch)
+                    for ref in here:
+                        t = ref_index[ref]
+                        L = int(reference_lengths[ref])
+                        closed = grouped and (nxt is None or int(nsel.ref_beg[t + 1]) == int(nsel.ref_beg[t]))
+                        reads = _indexed(ctx, bod.reads(t), L, scratch)
+                        b0 = int(sel.ref_beg[t])
+                        if closed and ref not in acc:  # the whole reference in this batch: fused
+                            results[ref], bad = _device_reference(
+                                ctx, reads, L, mbq, ncols, k, nf, nf2, _mode, tiles_of(ref),
+                                _tiles is not None, scratch)
+                            finished.add(ref)
+                        else:  # kernel 1 into the reference's accumulator
+                            if ref not in acc:
+                                acc[ref] = ctx.alloc(max(16, 4 * ncols * L))
+                                acc[ref].zero()
+                            ctx.count(reads, L, mbq, ncols, acc[ref].ptr)
+                            bad = ctx.range_error()
+                            if closed:
+                                results[ref] = _finish_reference(ctx, acc.pop(ref), L, ncols, k, nf, nf2, _mode,
+                                                                 tiles_of(ref), _tiles is not None, scratch)
+                                finished.add(ref)
+                        if bad >= 0 and ref not in fl.range_:
+                            fl.range_[ref] = (base + int(sel.ordinal[b0 + bad]),
+                                              _bad_pos(f, int(sel.rec[b0 + bad]), mbq, L))
+                    ctx.sync()  # the batch's host arrays may go once its copies are done
+                base += sel.n_accepted
+                cur.close()
+                cur, nxt = nxt, None
+            if ctx is not None and fl.inloop() is None:
+                for ref in mine:
+                    if ref in results:
+                        continue
                     L = int(reference_lengths[ref])
-                    results[ref], range_idx[ref] = _device_reference(
-                        ctx, _indexed(ctx, fod.reads(t), L, scratch), L, mbq, ncols, k, nf, nf2, _mode,
-                        _tiles(ref) if _tiles else None, _tiles is not None, scratch)
-            finally:
+                    if ref in acc:
+                        results[ref] = _finish_reference(ctx, acc.pop(ref), L, ncols, k, nf, nf2, _mode,
+                                                         tiles_of(ref), _tiles is not None, scratch)
+                    else:  # no reads at all
+                        results[ref], _ = _device_reference(ctx, _no_reads(), L, mbq, ncols, k, nf, nf2,
+                                                            _mode, tiles_of(ref), _tiles is not None, scratch)
+        finally:
+            for b in (cur, nxt):
+                if b is not None:
+                    b.close()
+            if ctx is not None:
                 ctx.sync()
+            for b in acc.values():
+                b.free()
+            if scratch is not None:
                 scratch.release()
-        if _group is not None and 0 <= mbq < _U32:
+        if _group is not None and mbq_ok:
             # every rank needs every reference's first out-of-range read to raise the same error
-            alls = _group.all_gather_ints([range_idx.get(r, -2) for r in ref_order])
-            range_idx = {r: alls[owner[r]][i] for i, r in enumerate(ref_order)}
-        err = _first_error(samfile, sel, ref_order, ref_index, reference_lengths, mbq,
-                           int(chunk_size), type_ord, range_idx)
+            flat = [v for r in ref_order for v in fl.range_.get(r, (-2, -1))]
+            alls = _group.all_gather_ints(flat)
+            fl.range_ = {}
+            for i, r in enumerate(ref_order):
+                o, bp = alls[owner[r]][2 * i], alls[owner[r]][2 * i + 1]
+                if o >= 0:
+                    fl.range_[r] = (o, bp)
+        err = _first_error(fl, ref_order, reference_lengths, mbq, int(chunk_size),
+                           _type_args(bam, B, mmq, wanted, ref_index))
         if err is not None:
             raise err
         out = {}
         for ref in mine:
-            t = ref_index[ref]
-            n = int(sel.ref_beg[t + 1] - sel.ref_beg[t])
+            n = nreads[ref]
             if _mode == "rows":
                 out[ref] = {"rows": Rows(ref, results[ref], long_format), "num_reads": n}
             else:
@@ -480,7 +627,14 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
             return out, owner, ref_order
         return out
     finally:
-        samfile.close()
+        stream.close()
+
+
+def _no_reads() -> D.BcReads:
+    r = D.BcReads()
+    r.sorted = 1
+    r.seq_layout = D.BC_SEQ_EVENT
+    return r
 
 
 def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
@@ -494,45 +648,75 @@ def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
 
 
 def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_tiles=False, scratch=None):
-    """Kernel 1 + kernel 2 (+ reductions) for one reference; returns (result, first bad read).
+    """Kernel 1 + kernel 2 (+ reductions) for one reference whose reads are all in ``reads``;
+    returns (result, first bad read of the batch).
 
-    Coordinate-sorted batches take the fused tiled kernel (bc_pileup); others count with the
-    event-parallel kernel (bc_count) and then run kernel 2 (bc_stats)."""
+    Coordinate-sorted batches take the fused pileup (bc_pileup / bc_pileup_summary); others
+    count with the event-parallel kernel (bc_count) and then run kernel 2 (bc_stats)."""
     if L == 0:
         if reads.n_reads > 0:
             hist = ctx.alloc(4 * ncols)
             hist.zero()
             ctx.count(reads, 0, mbq, ncols, hist.ptr)
         bad = ctx.range_error()
-        empty = RefData(np.zeros((k, 0), np.int32), np.zeros((k, 0)), np.zeros(0), np.zeros(0),
-                        np.zeros(0, np.int32))
-        return (empty if mode == "rows" else {"L": 0}), bad
+        return _empty(k, mode), bad
     scratch = scratch or _Scratch(ctx)
     outs = scratch.outputs(k, L, want_pc=(mode == "rows"))
     hist = scratch.get("hist", 4 * ncols * L)
     pc_ptr = outs["pc"].ptr if outs["pc"] else None
-    work = dout = None
-    if mode != "rows":
-        work = scratch.get("work", D.summary_work_bytes(L))
-        dout = scratch.get("dout", 32)
     if reads.sorted and mode != "rows":
         # pileup + summary: the sparse sweep computes numpy's buffer partials in registers
+        work, dout = scratch.get("work", D.summary_work_bytes(L)), scratch.get("dout", 32)
         ctx.pileup_summary(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr,
                            outs["ent"].ptr, outs["sec"].ptr, work.ptr, dout.ptr)
-    elif reads.sorted:
+        bad = ctx.range_error()
+        return _collect(ctx, outs, hist, L, k, ncols, mode, tiles, want_tiles, scratch, summarised=True), bad
+    if reads.sorted:
         ctx.pileup(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
                    outs["sec"].ptr)
-    else:
-        hist.zero(4 * ncols * L)
-        ctx.count(reads, L, mbq, ncols, hist.ptr)
-        ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, pc_ptr, outs["ent"].ptr,
-                  outs["sec"].ptr)
-        if mode != "rows":
-            ctx.summary(outs["cov"].ptr, outs["ent"].ptr, L, work.ptr, dout.ptr)
+        bad = ctx.range_error()
+        return _collect(ctx, outs, hist, L, k, ncols, mode, tiles, want_tiles, scratch, stats_done=True), bad
+    hist.zero(4 * ncols * L)
+    ctx.count(reads, L, mbq, ncols, hist.ptr)
     bad = ctx.range_error()
+    return _collect(ctx, outs, hist, L, k, ncols, mode, tiles, want_tiles, scratch), bad
+
+
+def _finish_reference(ctx, acc, L, ncols, k, nf, nf2, mode, tiles, want_tiles, scratch):
+    """Kernel 2 (+ reductions) for a reference whose counts were accumulated batch by batch in
+    the device histogram ``acc`` (freed here)."""
+    try:
+        if L == 0:
+            return _empty(k, mode)
+        outs = scratch.outputs(k, L, want_pc=(mode == "rows"))
+        return _collect(ctx, outs, acc, L, k, ncols, mode, tiles, want_tiles, scratch, nf=nf, nf2=nf2)
+    finally:
+        ctx.sync()
+        acc.free()
+
+
+def _empty(k, mode):
+    if mode != "rows":
+        return {"L": 0}
+    return RefData(np.zeros((k, 0), np.int32), np.zeros((k, 0)), np.zeros(0), np.zeros(0), np.zeros(0, np.int32))
+
+
+def _collect(ctx, outs, hist, L, k, ncols, mode, tiles, want_tiles, scratch, stats_done=False,
+             summarised=False, nf=None, nf2=None):
+    """The per-position statistics of the counts in ``hist`` (kernel 2, unless the fused pileup
+    already ran it), then either the rows (downloaded) or the summary and amplicon reductions."""
+    pc_ptr = outs["pc"].ptr if outs["pc"] else None
+    if not (stats_done or summarised):
+        if nf is None:
+            nf, nf2 = norm_factors(k)
+        ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, pc_ptr, outs["ent"].ptr, outs["sec"].ptr)
     if mode == "rows":
         counts = hist.download(np.int32, ncols * L).reshape(ncols, L)
-        return _download(outs, counts, k, L), bad
+        return _download(outs, counts, k, L)
+    dout = scratch.get("dout", 32)
+    if not summarised:
+        work = scratch.get("work", D.summary_work_bytes(L))
+        ctx.summary(outs["cov"].ptr, outs["ent"].ptr, L, work.ptr, dout.ptr)
     res = {"L": L}
     s = dout.download(np.float64, 4)
     res.update(avg_cov=np.float64(s[0]), avg_ent=np.float64(s[1]), nnz=int(s[2]))
@@ -549,7 +733,7 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
         res["amplicons"] = (amp, empty)
     elif want_tiles:
         res["amplicons"] = (np.zeros((0, 6)), [])
-    return res, bad
+    return res
 
 
 class BaseCount:

@@ -90,7 +90,12 @@ def test_c5_every_contig(ctx, c5):
         del hcov, hent
 
 
-def test_c5_cli_summarise(c5, tmp_path):
+@pytest.mark.parametrize("batch", [None, "200000"])
+def test_c5_cli_summarise(c5, tmp_path, monkeypatch, batch):
+    """batch 200000: the 1.2 M records stream in 6 batches; contigs cut by a batch boundary are
+    accumulated (bc_count per batch) and finished by kernel 2, the others take the fused sweep."""
+    if batch:
+        monkeypatch.setenv("BASECOUNT_BATCH_RECORDS", batch)
     bam = str(tmp_path / "c5.bam")
     synth.write_bam(c5, bam)
     got = _run_cli([bam, "--summarise"])
@@ -131,9 +136,13 @@ def test_c4_cli_summarise_with_bed(c3_bam, args, mbq, mmq):
         assert got == O.summary_text(f.references[0], exp, False, n, 3, tiles=tiles)
 
 
-def test_c3_cli_rows(c3_bam):
+@pytest.mark.parametrize("chunk", [None, "1000"])
+def test_c3_cli_rows(c3_bam, chunk):
+    """--chunk-size 1000: the reference flushes every 1000 reads (main.py:142-162); here the file
+    streams in 65,536-record batches (main.batch_records), 16 of them, each counted into the
+    reference's accumulator by the read-chunked kernel, then kernel 2 once."""
     bam, _ = c3_bam
-    got = _run_cli([bam])
+    got = _run_cli([bam] + (["--chunk-size", chunk] if chunk else []))
     with BamFile(bam) as f:
         b, _ = O.batch_from_bam(f, 0, 0)
         exp, (br, _) = O.bcount(f.lengths[0], 0, b)
@@ -144,9 +153,14 @@ def test_c3_cli_rows(c3_bam):
         assert got == header + O.rows_text(f.references[0], exp, False, False, 3)
 
 
-def test_unsorted_bam_cli_rows(tmp_path):
+@pytest.mark.parametrize("batch", [None, "7000"])
+def test_unsorted_bam_cli_rows(tmp_path, monkeypatch, batch):
     """An unsorted BAM (C2 shape, 3 contigs, reads in random order): the CLI takes the
-    event-parallel k_count + k_stats path; rows byte-identical to the oracle's main.py:454-466."""
+    event-parallel k_count + k_stats path; rows byte-identical to the oracle's main.py:454-466.
+    In 7000-record batches the contigs come back after a batch without them: the stream starts
+    again accumulating every contig to the end of the file (main._Ungrouped)."""
+    if batch:
+        monkeypatch.setenv("BASECOUNT_BATCH_RECORDS", batch)
     rs = synth.make_reads([("u1", 29_903), ("u2", 5_000), ("u3", 70_000)], 40_000, True, 91, unsorted=True)
     order = np.random.default_rng(5).permutation(rs.n)  # interleave the contigs too
     rs2 = synth.ReadSet(references=rs.references, lengths=rs.lengths, tid=rs.tid[order], pos=rs.pos[order],

@@ -589,7 +589,15 @@ def _run_cli(argv):
     return buf.getvalue()
 
 
-def test_cli_matches_reference_goldens(golden, manifest):
+# Streamed in batches far smaller than the file (main.batch_records): every reference of the
+# edge / error BAMs (<= 116 records, 4 references) crosses batch boundaries, faults land in
+# later batches, and c1 / mixed are counted by accumulation over 4-14 batches.
+def _stream_batches(bam: str) -> str:
+    return "3" if bam.startswith(("edge", "err")) else "300"
+
+
+@pytest.mark.parametrize("stream", [False, True])
+def test_cli_matches_reference_goldens(golden, manifest, monkeypatch, stream):
     n = 0
     cwd = os.getcwd()
     os.chdir(golden)
@@ -597,6 +605,8 @@ def test_cli_matches_reference_goldens(golden, manifest):
         for name, c in sorted(manifest.items()):
             if c.get("hashseed", "0") != "0" or name.startswith("err_order"):
                 continue  # set-order dependent: test_cli_hashseed_cases_byte_exact
+            if stream:
+                monkeypatch.setenv("BASECOUNT_BATCH_RECORDS", _stream_batches(c["bam"]))
             argv = [c["bam"]] + c["args"]
             summ = "--summarise" in c["args"] or "--summarise-with-bed" in c["args"]
             if c["returncode"] != 0:
@@ -623,13 +633,16 @@ def test_cli_matches_reference_goldens(golden, manifest):
     assert n >= 40
 
 
-def test_cli_hashseed_cases_byte_exact(golden, manifest):
+@pytest.mark.parametrize("stream", [False, True])
+def test_cli_hashseed_cases_byte_exact(golden, manifest, stream):
     """Multi-reference output order and first-error choice follow the set order (main.py:92)."""
     env0 = dict(os.environ, PYTHONPATH=REPO)
     for name, c in sorted(manifest.items()):
         if c.get("hashseed", "0") == "0" and not name.startswith(("edge_q0_m0", "err_order")):
             continue
         env = dict(env0, PYTHONHASHSEED=c.get("hashseed", "0"))
+        if stream:
+            env["BASECOUNT_BATCH_RECORDS"] = _stream_batches(c["bam"])
         p = subprocess.run([sys.executable, "-m", "basecount_amd", c["bam"]] + c["args"],
                            cwd=golden, env=env, capture_output=True, timeout=300)
         if c["returncode"] != 0:

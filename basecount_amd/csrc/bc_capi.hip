@@ -419,6 +419,40 @@ int bc_reads_index(bc_ctx* c, bc_reads* r, int64_t L, int what, void* d_mem, siz
     return BC_OK;
 }
 
+int bc_reads_sort_bytes(bc_ctx* c, const bc_reads* r, size_t* bytes) {
+    if (!c || !r || !bytes) return fail(BC_E_ARG, "NULL argument");
+    *bytes = bc::sort_bytes(*r);
+    return BC_OK;
+}
+
+int bc_reads_sort(bc_ctx* c, const bc_reads* r, bc_reads* out, void* d_mem, size_t bytes) {
+    if (!c || !r || !out) return fail(BC_E_ARG, "NULL argument");
+    if (r->n_reads < 0 || r->max_end < 0) return fail(BC_E_ARG, "bc_reads_sort: negative n_reads / max_end");
+    if (r->n_reads >= (int64_t)0xFFFFFFFF) return fail(BC_E_ARG, "bc_reads_sort: more than 2^32 - 1 reads");
+    if (r->n_reads == 0) {
+        *out = *r;
+        out->sorted = 1;
+        return BC_OK;
+    }
+    if (r->seq_layout != BC_SEQ_EVENT) return fail(BC_E_ARG, "bc_reads_sort needs seq_layout == BC_SEQ_EVENT");
+    if (!r->pos || !r->cig_beg || !r->cig_n || !r->seq_nib || !r->seq) return fail(BC_E_ARG, "bc_reads_sort: missing array");
+    const size_t need = bc::sort_bytes(*r);
+    if (!d_mem || bytes < need) return fail(BC_E_ARG, "bc_reads_sort: d_mem smaller than bc_reads_sort_bytes");
+    if ((uintptr_t)d_mem & 255u) return fail(BC_E_ARG, "bc_reads_sort: d_mem must be 256-byte aligned");
+    DeviceGuard g(c->device);
+    bc_reads tmp;
+    {
+        Timed tm(c, BC_K_SORT);
+        HIP_TRY(bc::launch_sort(c->stream, *r, tmp, d_mem));
+    }
+    uint32_t overflow = 0;
+    HIP_TRY(hipMemcpyAsync(&overflow, bc::sort_overflow_word(*r, d_mem), 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (overflow) return fail(BC_E_ARG, "bc_reads_sort: the reads' sequences overlap (sorted copy would not fit)");
+    *out = tmp;
+    return BC_OK;
+}
+
 int bc_reads_free(bc_ctx* c, bc_reads* d) {
     if (!c || !d) return fail(BC_E_ARG, "NULL argument");
     DeviceGuard g(c->device);

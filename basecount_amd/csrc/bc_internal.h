@@ -92,6 +92,13 @@ inline bool pileup_is_solo(const bc_reads& r, int64_t L, int shape, int tile_wav
     return shape != BC_SHAPE_TILE_NO_SOLO && pileup_waves(r, L, r.max_end, tile_waves) == 1;
 }
 
+// ---- the coordinate-sorted copy of an unsorted batch (bc_sort.hip) ----
+size_t sort_bytes(const bc_reads& r);
+// enqueues the sort into mem (sort_bytes(r) bytes) and fills `out` (sorted, no index)
+hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem);
+// device word set when the sorted sequence would not fit its buffer (read after a sync)
+const uint32_t* sort_overflow_word(const bc_reads& r, void* mem);
+
 // ---- the device index of a sorted batch (bc_index.hip) ----
 // bc_reads.index_tag: the batch identity an index was built for (never 0)
 inline uint64_t index_tag(const bc_reads& r) {

@@ -1,0 +1,288 @@
+// bc_sort.hip — a coordinate-sorted copy of an unsorted batch, built on the device.
+//
+// The reference consumes reads in file order (main.py:127); counts do not depend on the order
+// (count.cpp:22-97 adds one per event), but the fast kernels do: the tiled k_pileup walks a
+// contiguous range of reads per tile and the read-chunked k_rc stages a chunk's contiguous
+// sequence.  An unsorted batch (reads of one reference in any order) is therefore put in start
+// order here, with no host round trip:
+//   1. k_sort_count    counting sort by start position: one atomic per read on its position's bin
+//                      (the returned old value is the read's rank inside the bin), and the
+//                      read's query length from its CIGAR (M/I/=/X);
+//   2. scan_u32        exclusive prefix sum of the bins (3 launches: tile sums, their scan, add);
+//   3. k_sort_scatter  each read's fields to its sorted slot, with the bytes of sequence it needs;
+//   4. scan_u32        of those bytes: the sorted sequence buffer's offsets;
+//   5. k_sort_seq      each read's aligned sequence (and its qualities) copied to its offset, so
+//                      a chunk of sorted reads has one contiguous sequence segment again.
+// The CIGAR buffer is shared with the input (reads keep their cig_beg).  HBM traffic ~ 2x the
+// batch's sequence + 40 B per read; every pass is a streaming, fully parallel kernel.
+#include "bc_internal.h"
+
+namespace bc {
+namespace {
+
+#include "bc_runs.h"
+
+constexpr int kScanTile = 1024;  // elements per scan block (256 threads x 4)
+
+__global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* a, int64_t m, uint32_t* sums) {
+    __shared__ uint32_t ws[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile + 4 * threadIdx.x;
+    uint32_t v[4], t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = base + k < m ? a[base + k] : 0u;
+        t += v[k];
+    }
+    // inclusive scan of the thread totals: wave (DPP-free shuffles), then across the 4 waves
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += ws[w];
+    uint32_t run = before + inc - t;  // exclusive prefix of this thread's first element
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (base + k < m) a[base + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 255) sums[blockIdx.x] = before + inc;
+}
+
+// one block: exclusive scan of the tile sums in place (any count, 1024 per pass with a carry)
+__global__ __launch_bounds__(256) void k_scan_sums(uint32_t* sums, int64_t n, uint32_t* total) {
+    __shared__ uint32_t ws[4];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t b0 = 0; b0 < n; b0 += kScanTile) {
+        const int64_t base = b0 + 4 * threadIdx.x;
+        uint32_t v[4], t = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = base + k < n ? sums[base + k] : 0u;
+            t += v[k];
+        }
+        uint32_t inc = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) ws[wave] = inc;
+        __syncthreads();
+        uint32_t before = carry;
+        for (int w = 0; w < wave; ++w) before += ws[w];
+        uint32_t run = before + inc - t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (base + k < n) sums[base + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        if (threadIdx.x == 255) carry = before + inc;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(uint32_t* a, int64_t m, const uint32_t* sums) {
+    const int64_t base = (int64_t)blockIdx.x * kScanTile + 4 * threadIdx.x;
+    const uint32_t add = sums[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + k < m) a[base + k] += add;
+}
+
+// exclusive prefix sum of a[0, m) in place; tmp holds scan_tmp_words(m) words; *total (device,
+// may be NULL) = the sum of all elements
+size_t scan_tmp_words(int64_t m) { return (size_t)((m + kScanTile - 1) / kScanTile) + 1; }
+
+hipError_t scan_u32(hipStream_t s, uint32_t* a, int64_t m, uint32_t* tmp, uint32_t* total) {
+    const int64_t tiles = (m + kScanTile - 1) / kScanTile;
+    if (tiles == 0) return total ? hipMemsetAsync(total, 0, 4, s) : hipSuccess;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(256), 0, s, a, m, tmp);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, tmp, tiles, total);
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)tiles), dim3(256), 0, s, a, m, (const uint32_t*)tmp);
+    return hipGetLastError();
+}
+
+struct SortArgs {
+    const int32_t* pos;
+    const uint32_t* cig_beg;
+    const uint32_t* cig_n;
+    const uint32_t* seq_nib;
+    const uint32_t* cigar;
+    const uint8_t* seq;
+    const uint8_t* qual;
+    int64_t n;
+    uint32_t* bins;   // [nbins] counts, then offsets
+    uint32_t* rank;   // [n] rank of read i inside its bin
+    uint32_t* qlen;   // [n] query bases of read i (M/I/=/X)
+    uint32_t* src;    // [n] source nibble index of sorted read j
+    int32_t* o_pos;
+    uint32_t* o_cig_beg;
+    uint32_t* o_cig_n;
+    uint32_t* o_seq_nib;
+    uint32_t* o_bytes;  // sequence bytes of sorted read j, then their offsets
+    uint32_t* total;    // sum of o_bytes (device word)
+    uint32_t* overflow; // set when the sorted sequence would not fit cap bytes
+    uint8_t* o_seq;
+    uint8_t* o_qual;
+    uint32_t cap;       // bytes of o_seq (o_qual: twice as many)
+};
+
+__global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.n) return;
+    A.rank[i] = atomicAdd(&A.bins[A.pos[i]], 1u);
+    const uint32_t* cg = A.cigar + A.cig_beg[i];
+    uint32_t q = 0;
+    for (uint32_t k = 0, cn = A.cig_n[i]; k < cn; ++k) {
+        const uint32_t w = cg[k];
+        if (qcons(w & 15u)) q += w >> 4;
+    }
+    A.qlen[i] = q;
+}
+
+__global__ __launch_bounds__(256) void k_sort_scatter(SortArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.n) return;
+    const uint32_t j = A.bins[A.pos[i]] + A.rank[i];
+    const uint32_t sn = A.seq_nib[i];
+    A.o_pos[j] = A.pos[i];
+    A.o_cig_beg[j] = A.cig_beg[i];
+    A.o_cig_n[j] = A.cig_n[i];
+    A.src[j] = sn;
+    A.o_bytes[j] = ((sn & 1u) + A.qlen[i] + 1u) >> 1;  // the whole bytes holding its aligned bases
+}
+
+// 16 lanes per sorted read: its bytes of sequence (and the two quality bytes of each) copied to
+// its offset, lane-strided; the new nibble index keeps the old one's parity
+__global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
+    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const uint32_t sub = threadIdx.x & 15u;
+    if (j >= A.n) return;
+    const uint32_t sn = A.src[j], off = A.o_bytes[j];
+    const uint32_t end = j + 1 < A.n ? A.o_bytes[j + 1] : *A.total;
+    if ((uint64_t)end > (uint64_t)A.cap || end < off) {
+        if (sub == 0) atomicOr(A.overflow, 1u);
+        return;
+    }
+    const uint32_t from = sn >> 1, len = end - off;
+    for (uint32_t k = sub; k < len; k += 16) A.o_seq[off + k] = A.seq[from + k];
+    if (A.qual)
+        for (uint32_t k = sub; k < 2 * len; k += 16) A.o_qual[2 * (uint64_t)off + k] = A.qual[2 * (uint64_t)from + k];
+    if (sub == 0) A.o_seq_nib[j] = 2 * off + (sn & 1u);
+}
+
+struct SortLayout {
+    size_t bins, rank, qlen, src, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, total;
+    int64_t nbins;
+    uint32_t cap;
+};
+
+SortLayout sort_layout(const bc_reads& r) {
+    SortLayout L{};
+    const int64_t n = r.n_reads;
+    L.nbins = r.max_end + 2;  // every start <= max_end
+    L.cap = (uint32_t)std::min<int64_t>(r.seq_bytes + n + 16, 0xFFFFFFF0ll);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = off;
+        off += (bytes + 255) / 256 * 256;
+        return at;
+    };
+    L.bins = take(4 * (size_t)L.nbins);
+    L.rank = take(4 * (size_t)n);
+    L.qlen = take(4 * (size_t)n);
+    L.src = take(4 * (size_t)n);
+    L.o_pos = take(4 * (size_t)n);
+    L.o_cb = take(4 * (size_t)n);
+    L.o_cn = take(4 * (size_t)n);
+    L.o_sn = take(4 * (size_t)n);
+    L.o_bytes = take(4 * (size_t)n + 4);
+    L.tmp = take(4 * scan_tmp_words(std::max<int64_t>(L.nbins, n)));
+    L.words = take(16);  // total, overflow
+    L.o_seq = take(seq_event_bytes(L.cap));
+    L.o_qual = r.qual ? take(2 * (size_t)L.cap + 32) : 0;
+    L.total = off;
+    return L;
+}
+
+}  // namespace
+
+size_t sort_bytes(const bc_reads& r) {
+    if (r.n_reads <= 0) return 0;
+    return sort_layout(r).total;
+}
+
+hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem) {
+    const SortLayout L = sort_layout(r);
+    uint8_t* b = (uint8_t*)mem;
+    SortArgs A;
+    A.pos = r.pos;
+    A.cig_beg = r.cig_beg;
+    A.cig_n = r.cig_n;
+    A.seq_nib = r.seq_nib;
+    A.cigar = r.cigar;
+    A.seq = r.seq;
+    A.qual = r.qual;
+    A.n = r.n_reads;
+    A.bins = (uint32_t*)(b + L.bins);
+    A.rank = (uint32_t*)(b + L.rank);
+    A.qlen = (uint32_t*)(b + L.qlen);
+    A.src = (uint32_t*)(b + L.src);
+    A.o_pos = (int32_t*)(b + L.o_pos);
+    A.o_cig_beg = (uint32_t*)(b + L.o_cb);
+    A.o_cig_n = (uint32_t*)(b + L.o_cn);
+    A.o_seq_nib = (uint32_t*)(b + L.o_sn);
+    A.o_bytes = (uint32_t*)(b + L.o_bytes);
+    A.total = (uint32_t*)(b + L.words);
+    A.overflow = A.total + 1;
+    A.o_seq = b + L.o_seq;
+    A.o_qual = r.qual ? b + L.o_qual : nullptr;
+    A.cap = L.cap;
+    uint32_t* tmp = (uint32_t*)(b + L.tmp);
+    const unsigned blocks = (unsigned)((r.n_reads + 255) / 256);
+    hipError_t e = hipMemsetAsync(A.bins, 0, 4 * (size_t)L.nbins, s);
+    if (e == hipSuccess) e = hipMemsetAsync(A.total, 0, 16, s);
+    // the sorted sequence's padding (BC_SEQ_EVENT) is zero
+    if (e == hipSuccess) e = hipMemsetAsync(A.o_seq, 0, seq_event_bytes(L.cap), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sort_count, dim3(blocks), dim3(256), 0, s, A);
+    if ((e = scan_u32(s, A.bins, L.nbins, tmp, nullptr)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sort_scatter, dim3(blocks), dim3(256), 0, s, A);
+    if ((e = scan_u32(s, A.o_bytes, r.n_reads, tmp, A.total)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sort_seq, dim3((unsigned)((r.n_reads * 16 + 255) / 256)), dim3(256), 0, s, A);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    out = r;
+    out.pos = A.o_pos;
+    out.cig_beg = A.o_cig_beg;
+    out.cig_n = A.o_cig_n;
+    out.seq_nib = A.o_seq_nib;
+    out.seq = A.o_seq;
+    out.seq_bytes = L.cap;
+    out.qual = A.o_qual;
+    out.qual_bytes = r.qual ? 2 * (int64_t)L.cap : 0;
+    out.sorted = 1;
+    out.seq_layout = BC_SEQ_EVENT;
+    out.read_runs = nullptr;
+    out.run_chunks = 0;
+    out.tile_reads = nullptr;
+    out.n_tiles = 0;
+    out.index_tag = 0;
+    return hipSuccess;
+}
+
+const uint32_t* sort_overflow_word(const bc_reads& r, void* mem) {
+    return (const uint32_t*)((uint8_t*)mem + sort_layout(r).words) + 1;
+}
+
+}  // namespace bc

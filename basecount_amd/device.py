@@ -18,7 +18,7 @@ BC_E_ARG, BC_E_HIP, BC_E_RANGE, BC_E_NODEV, BC_E_COMM = -1, -2, -3, -4, -5
 COMM_ID_BYTES = 128  # BC_COMM_ID_BYTES
 BC_SEQ_BAM, BC_SEQ_EVENT = 0, 1
 SHAPES = {"auto": 0, "tile": 1, "rc": 2, "tile_no_solo": 3}  # BC_SHAPE_*
-KERNEL_NAMES = ("count", "stats", "rc", "pileup", "summary", "amplicons", "index", "solo")  # BC_K_* ids
+KERNEL_NAMES = ("count", "stats", "rc", "pileup", "summary", "amplicons", "index", "solo", "sort")  # BC_K_* ids
 BC_INDEX_RUNS, BC_INDEX_TILES, BC_INDEX_AUTO = 1, 2, 4
 KERNEL_IDS = len(KERNEL_NAMES)
 
@@ -79,6 +79,8 @@ def lib() -> C.CDLL:
         "bc_reads_free": ([vp, C.POINTER(BcReads)], C.c_int),
         "bc_reads_index_bytes": ([vp, C.POINTER(BcReads), i64, C.c_int, C.POINTER(C.c_size_t)], C.c_int),
         "bc_reads_index": ([vp, C.POINTER(BcReads), i64, C.c_int, vp, C.c_size_t], C.c_int),
+        "bc_reads_sort_bytes": ([vp, C.POINTER(BcReads), C.POINTER(C.c_size_t)], C.c_int),
+        "bc_reads_sort": ([vp, C.POINTER(BcReads), C.POINTER(BcReads), vp, C.c_size_t], C.c_int),
         "bc_count": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, vp], C.c_int),
         "bc_range_error": ([vp, C.POINTER(i64)], C.c_int),
         "bc_stats": ([vp, vp, i64, C.c_int, dbl, dbl, vp, vp, vp, vp], C.c_int),
@@ -283,6 +285,21 @@ class Context:
         index) into d_mem on the stream and set the index fields of the bc_reads in place."""
         r = reads.r if isinstance(reads, DeviceReads) else reads
         check(lib().bc_reads_index(self.h, C.byref(r), int(L), int(what), d_mem, int(nbytes)))
+
+    def sort_bytes(self, reads) -> int:
+        """bc_reads_sort_bytes: device bytes the sorted copy of an unsorted batch needs."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        n = C.c_size_t(0)
+        check(lib().bc_reads_sort_bytes(self.h, C.byref(r), C.byref(n)))
+        return int(n.value)
+
+    def sort(self, reads, d_mem, nbytes: int) -> BcReads:
+        """bc_reads_sort: a coordinate-sorted copy of the batch, built on the device into d_mem
+        (blocking); returns its bc_reads (no index yet)."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        out = BcReads()
+        check(lib().bc_reads_sort(self.h, C.byref(r), C.byref(out), d_mem, int(nbytes)))
+        return out
 
     def pileup(self, reads, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec):
         """Fused kernel 1 + kernel 2 (bc_pileup) for a coordinate-sorted batch: one launch."""

@@ -638,9 +638,13 @@ def _no_reads() -> D.BcReads:
 
 
 def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
-    """The device index the kernels would use for this slice (bc_reads_index, BC_INDEX_AUTO:
-    run records + chunk summaries for the read-chunked kernel, the tile index for the tiled
-    one), built on the device into the reusable scratch, stream-ordered before the kernels."""
+    """The slice as the fast kernels take it: an unsorted slice is first put in start order on
+    the device (bc_reads_sort, into the reusable scratch), then the device index the kernels
+    would use (bc_reads_index, BC_INDEX_AUTO: run records + chunk summaries for the read-chunked
+    kernel, the tile index for the tiled one), stream-ordered before the kernels."""
+    if not reads.sorted and reads.n_reads > 1:
+        nb = ctx.sort_bytes(reads)
+        reads = ctx.sort(reads, scratch.get("sorted", nb).ptr, nb)
     nb = ctx.index_bytes(reads, L)
     if nb:
         ctx.index(reads, L, scratch.get("index", nb).ptr, nb)

@@ -634,6 +634,78 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     return res
 
 
+def run_unsorted(ctx, args, reps: int = 20) -> dict:
+    """C3's reads in random order (an unsorted BAM's batch, main.py:127 consumes file order):
+    the event-parallel k_count (+ k_stats) path against the device sort (bc_reads_sort: counting
+    sort by start + sequence relayout) followed by the sorted path (index + k_rc + k_stats).
+    Each step starts from the raw unsorted batch in HBM; parity of both against the oracle."""
+    import oracle as O
+    from basecount_amd import device as D
+    from basecount_amd import synth
+    from basecount_amd.bam import seq_to_event
+    from basecount_amd.main import norm_factors
+
+    rs = synth.make_config("c3", unsorted=True)
+    b = synth.batch_arrays(rs, 0, 0)
+    L, k = rs.lengths[0], 5
+    nf, nf2 = norm_factors(k)
+    reads = D.DeviceReads(ctx, dict(b, qual=None, seq_event=seq_to_event(b["seq"])))
+    assert reads.r.sorted == 0
+    counts, cov, pc = ctx.alloc(4 * k * L), ctx.alloc(4 * L), ctx.alloc(8 * k * L)
+    ent, sec = ctx.alloc(8 * L), ctx.alloc(8 * L)
+    nb = ctx.sort_bytes(reads)
+    mem = ctx.alloc(nb)
+
+    def event_parallel():
+        counts.zero()
+        ctx.count(reads, L, 0, k, counts.ptr)
+        ctx.stats(counts.ptr, L, k, nf, nf2, cov.ptr, pc.ptr, ent.ptr, sec.ptr)
+
+    def region(fn, n):
+        ctx.sync()
+        ctx.event_record(2)
+        for _ in range(n):
+            fn()
+        ctx.event_record(3)
+        return ctx.event_elapsed_ms(2, 3) * 1e3 / n
+
+    for _ in range(3):
+        event_parallel()
+    ep_us = region(event_parallel, reps)
+    exp, _ = O.bcount(L, 0, b, nthreads=cpu_threads())
+    ok_ep = bool(np.array_equal(counts.download(np.int32, k * L).reshape(k, L), exp[:, :k].T.astype(np.int32)))
+    # the sorted path: the sort's own device time (library timing facility: the call blocks), then
+    # index + k_rc + k_stats on the sorted copy
+    srt = ctx.sort(reads, mem.ptr, nb)
+    ctx.timing(True)
+    for _ in range(reps):
+        srt = ctx.sort(reads, mem.ptr, nb)
+    sort_us = ctx.timing_report()["sort"][1]
+    ctx.timing(False)
+    inb = ctx.index_bytes(srt, L)
+    imem = ctx.alloc(max(16, inb))
+
+    def sorted_step():
+        if inb:
+            ctx.index(srt, L, imem.ptr, inb)
+        ctx.pileup(srt, L, 0, k, nf, nf2, counts.ptr, cov.ptr, pc.ptr, ent.ptr, sec.ptr)
+
+    for _ in range(3):
+        sorted_step()
+    ss_us = region(sorted_step, reps)
+    ok_s = bool(np.array_equal(counts.download(np.int32, k * L).reshape(k, L), exp[:, :k].T.astype(np.int32)))
+    for x in (counts, cov, pc, ent, sec, mem, imem):
+        x.free()
+    reads.free()
+    return {"workload": "C3 reads in random order (unsorted batch, 1,000,000 mixed-CIGAR reads, 29,903 bp)",
+            "event_parallel_step_us": ep_us,
+            "event_parallel": "k_count (event-parallel kernel 1, global atomics) + k_stats, from the unsorted batch",
+            "sort_us": sort_us, "sorted_step_us": ss_us, "sort_then_sorted_path_us": sort_us + ss_us,
+            "sorted_path": "bc_reads_sort (counting sort by start + sequence relayout, device) then "
+                           "k_index_runs + k_rc + k_stats",
+            "parity_vs_oracle": ok_ep and ok_s}
+
+
 def _free_port() -> int:
     import socket
 
@@ -794,6 +866,8 @@ def main():
             r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=(cfg == "c5"))
             r.pop("_wl").free()
             extra[cfg] = r
+        if world == 1:
+            extra["c3_unsorted"] = run_unsorted(ctx, args)
 
     cpu = cpu_all = e2e_res = None
     if rank == 0 and world == 1:

@@ -171,6 +171,19 @@ int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
  * launches the build on the context's stream (async, no allocation: capturable) and sets the
  * index fields and index_tag of *d_reads.  d_reads->sorted / max_span / max_end must be
  * truthful.  bc_reads_upload builds BC_INDEX_AUTO for ref_len = max_end into its own slab.    */
+/* A coordinate-sorted copy of an unsorted device batch, built on the device (bc_sort.hip):
+ * a counting sort of the reads by start position, their per-read arrays written in that order
+ * and each read's aligned sequence (and qualities) copied so that consecutive reads have
+ * consecutive sequence again.  The copy shares d_reads' CIGAR buffer; everything else lives in
+ * d_mem (bc_reads_sort_bytes bytes, 256-byte aligned), which must outlive its use.  *d_sorted
+ * is then a sorted batch (sorted = 1, same max_span / max_end, no index: build one with
+ * bc_reads_index) that every kernel takes, with the same counts as the input (count.cpp's sums
+ * do not depend on the read order).  Needs d_reads->max_end truthful and seq_layout ==
+ * BC_SEQ_EVENT; the reads' aligned sequences must not overlap (true of any decoded batch).
+ * Blocking: returns after the copy is complete (BC_E_ARG if the sequences did overlap).      */
+int bc_reads_sort_bytes(bc_ctx* ctx, const bc_reads* d_reads, size_t* bytes);
+int bc_reads_sort(bc_ctx* ctx, const bc_reads* d_reads, bc_reads* d_sorted, void* d_mem, size_t bytes);
+
 #define BC_INDEX_RUNS 1
 #define BC_INDEX_TILES 2
 #define BC_INDEX_AUTO 4
@@ -234,7 +247,8 @@ int bc_ctx_wait(bc_ctx* ctx, bc_ctx* other);
 #define BC_K_AMPLICONS 5
 #define BC_K_INDEX 6      /* the device index build (bc_reads_index / bc_reads_upload)  */
 #define BC_K_SOLO 7       /* the sparse sweep k_pileup_solo (fused kernel 1 + 2)     */
-#define BC_KERNEL_IDS 8
+#define BC_K_SORT 8       /* the device sort of an unsorted batch (bc_reads_sort)     */
+#define BC_KERNEL_IDS 9
 int bc_timing_enable(bc_ctx* ctx, int on);
 int bc_timing_report(bc_ctx* ctx, int64_t* launches /* [BC_KERNEL_IDS] */, double* mean_us /* [..] */);
 

@@ -330,6 +330,42 @@ def test_reads_index_on_device_slices(ctx, shape):
     whole.free()
 
 
+@pytest.mark.parametrize("seed,L,n,mbq", [(71, 3_000, 20_000, 0), (72, 30_000, 60_000, 20), (73, 500, 5, 0),
+                                          (74, 2_000_000, 3_000, 40), (75, 6_000, 40_000, 20)])
+def test_device_sort_of_unsorted_batch(ctx, seed, L, n, mbq):
+    """bc_reads_sort: an unsorted batch put in start order on the device (counting sort + the
+    sequence / quality relayout); the sorted copy's starts are non-decreasing, it keeps every
+    read, and every kernel shape on it gives the unsorted batch's counts (count.cpp's sums do
+    not depend on the order)."""
+    rng = np.random.default_rng(seed)
+    b = random_batch(rng, L, n, sort=False)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    r = D.DeviceReads(ctx, b)
+    nb = ctx.sort_bytes(r)
+    mem = ctx.alloc(nb)
+    s = ctx.sort(r, mem.ptr, nb)
+    assert s.sorted == 1 and s.n_reads == r.r.n_reads
+    pos = np.zeros(s.n_reads, np.int32)
+    D.check(D.lib().bc_memcpy_d2h(ctx.h, pos.ctypes.data, s.pos, pos.nbytes))
+    ctx.sync()
+    assert np.all(pos[1:] >= pos[:-1]) and np.array_equal(np.sort(b["pos"]), pos)
+    for shape in ("auto", "tile_no_solo", "rc", "tile"):
+        ctx.set_shape(shape)
+        for k in (5, 6):
+            nbi = ctx.index_bytes(s, L)
+            imem = ctx.alloc(max(16, nbi))
+            if nbi:
+                ctx.index(s, L, imem.ptr, nbi)
+            hist = ctx.alloc(4 * k * L)
+            hist.zero()
+            ctx.count(s, L, mbq, k, hist.ptr)
+            assert ctx.range_error() == -1
+            got = hist.download(np.int32, k * L).reshape(k, L)
+            assert np.array_equal(got, exp[:, :k].T.astype(np.int32)), (shape, k)
+    r.free()
+
+
 def test_rc_event_image_range_error(ctx):
     """A read running past the reference end inside an imaged chunk: the reference's first
     offending read (std::out_of_range), nothing counted past L."""

@@ -118,7 +118,7 @@ private:
 // Read-only mapping of the BAM file (read() into a buffer only if mmap is refused).
 class FileMap {
 public:
-    int open(const char* path) {
+    int open(const char* path, bool sequential = false) {
         int fd = ::open(path, O_RDONLY | O_CLOEXEC);
         if (fd < 0) return -1;
         struct stat st;
@@ -130,7 +130,7 @@ public:
         if (n_) {
             void* m = mmap(nullptr, n_, PROT_READ, MAP_PRIVATE, fd, 0);
             if (m != MAP_FAILED) {
-                madvise(m, n_, MADV_WILLNEED);
+                madvise(m, n_, sequential ? MADV_SEQUENTIAL : MADV_WILLNEED);
                 map_ = (const uint8_t*)m;
             } else {
                 buf_.resize(n_);
@@ -158,6 +158,10 @@ public:
     }
     const uint8_t* data() const { return map_ ? map_ : buf_.data(); }
     size_t size() const { return n_; }
+    // give pages of [off, off + len) back (page-aligned off); the mapping stays valid
+    void drop(size_t off, size_t len) {
+        if (map_ && len) madvise((void*)(map_ + off), len, MADV_DONTNEED);
+    }
 
 private:
     const uint8_t* map_ = nullptr;
@@ -437,24 +441,19 @@ int parse_header(const uint8_t* p, uint64_t N, std::vector<std::string>& names, 
 
 }  // namespace
 
-// Records from p[q0, N) into f's struct of arrays: at most max_records complete records.  With
-// partial_ok a truncated record at the end is left for a later call (*q_end = its offset);
-// without, it is a format error.  One hop over the record lengths records the starts and the
-// prefix sums of cigar / seq sizes (prefetching ahead of its load chain), then a parallel fill.
-int decode_records(bcio_file* f, const uint8_t* p, uint64_t q0, uint64_t N, int64_t max_records, bool partial_ok,
-                   int nthreads, uint64_t* q_end, PhaseTimer* pt) {
-    constexpr uint64_t kPf = 4096;
-    uint64_t q = q0;
+// The hop over record lengths: starts of the complete records and the prefix sums of their cigar
+// / seq sizes, continued from where it stopped (q) at each call.  With partial_ok a truncated
+// record at the end waits for more bytes; without, it is a format error.
+struct Hop {
     uvec<uint64_t> starts;
-    starts.reserve(std::max<uint64_t>(16, std::min<uint64_t>((N - q) / 256, (uint64_t)std::max<int64_t>(16, max_records))));
-    f->cig_off.clear();
-    f->seq_off.clear();
-    f->cig_off.reserve(starts.capacity() + 1);
-    f->seq_off.reserve(starts.capacity() + 1);
-    f->cig_off.push_back(0);
-    f->seq_off.push_back(0);
-    uint64_t cig_tot = 0, seq_tot = 0, pf = q;
-    while (q < N && (int64_t)starts.size() < max_records) {
+    uvec<uint64_t> cig_off{0}, seq_off{0};
+    uint64_t q = 0, cig_tot = 0, seq_tot = 0, pf = 0;
+};
+
+int hop_records(Hop& h, const uint8_t* p, uint64_t N, int64_t max_records, bool partial_ok) {
+    constexpr uint64_t kPf = 4096;  // prefetch distance: the hop's dependent loads become a stream
+    uint64_t q = h.q;
+    while (q < N && (int64_t)h.starts.size() < max_records) {
         if (q + 4 > N) {
             if (partial_ok) break;
             return fail(BCIO_E_FORMAT, "truncated record length");
@@ -466,21 +465,47 @@ int decode_records(bcio_file* f, const uint8_t* p, uint64_t q0, uint64_t N, int6
             return fail(BCIO_E_FORMAT, "truncated BAM record");
         }
         const uint64_t pf_end = std::min(N, q + 4 + bs + kPf);
-        for (pf = std::max(pf, q + kPf); pf < pf_end; pf += 64) __builtin_prefetch(p + pf);
+        for (h.pf = std::max(h.pf, q + kPf); h.pf < pf_end; h.pf += 64) __builtin_prefetch(p + h.pf);
         const uint8_t* r = p + q + 4;
         int32_t ls = rd32s(r + 16);
         if (ls < 0) return fail(BCIO_E_FORMAT, "negative l_seq");
         // the fields must fit the record before their sizes feed the output allocations
         if (32ull + r[8] + 4ull * rd16(r + 12) + (((uint64_t)ls + 1) / 2) + (uint64_t)ls > bs)
             return fail(BCIO_E_FORMAT, "BAM record shorter than its fields");
-        starts.push_back(q);
-        cig_tot += rd16(r + 12);
-        seq_tot += (((uint64_t)ls + 1) / 2);
-        f->cig_off.push_back(cig_tot);
-        f->seq_off.push_back(seq_tot);
+        h.starts.push_back(q);
+        h.cig_tot += rd16(r + 12);
+        h.seq_tot += (((uint64_t)ls + 1) / 2);
+        h.cig_off.push_back(h.cig_tot);
+        h.seq_off.push_back(h.seq_tot);
         q += 4 + (uint64_t)bs;
     }
-    *q_end = q;
+    h.q = q;
+    return BCIO_OK;
+}
+
+int fill_records(bcio_file* f, const uint8_t* p, Hop& h, int nthreads, PhaseTimer* pt);
+
+// Records from p[q0, N) into f's struct of arrays: at most max_records complete records (see
+// hop_records), then a parallel fill; *q_end = the offset after the last one.
+int decode_records(bcio_file* f, const uint8_t* p, uint64_t q0, uint64_t N, int64_t max_records, bool partial_ok,
+                   int nthreads, uint64_t* q_end, PhaseTimer* pt) {
+    Hop h;
+    h.q = h.pf = q0;
+    const uint64_t guess = std::max<uint64_t>(16, std::min<uint64_t>((N - q0) / 256, (uint64_t)std::max<int64_t>(16, max_records)));
+    h.starts.reserve(guess);
+    h.cig_off.reserve(guess + 1);
+    h.seq_off.reserve(guess + 1);
+    int rc = hop_records(h, p, N, max_records, partial_ok);
+    if (rc != BCIO_OK) return rc;
+    *q_end = h.q;
+    return fill_records(f, p, h, nthreads, pt);
+}
+
+int fill_records(bcio_file* f, const uint8_t* p, Hop& h, int nthreads, PhaseTimer* pt) {
+    uvec<uint64_t>& starts = h.starts;
+    const uint64_t cig_tot = h.cig_tot, seq_tot = h.seq_tot;
+    f->cig_off.swap(h.cig_off);
+    f->seq_off.swap(h.seq_off);
     const int64_t n = (int64_t)starts.size();
     f->tid.resize(n);
     f->pos.resize(n);
@@ -752,56 +777,42 @@ extern "C" int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_se
 }
 
 // ------------------------------------------------------------------------------------------
-// streaming decode (bounded memory): the file is read with pread in compressed slabs, the slab's
-// complete BGZF blocks are inflated in parallel onto the pending bytes, and each call hands out
-// the next max_records complete records as their own bcio_file.  Live memory: one batch, one
-// compressed slab and the inflated bytes not yet handed out (< one slab's worth beyond the batch).
+// streaming decode (bounded memory).  The file is mapped read-only; each fill scans BGZF block
+// headers ahead until the blocks hold the bytes the batch is estimated to need (from the
+// records' mean size so far), inflates all of them in ONE parallel pass into a buffer sized
+// once (the carried partial record first), and drops the consumed part of the mapping
+// (MADV_DONTNEED), so resident memory is one batch plus its inflated bytes, never the file.
 struct bcio_stream {
-    int fd = -1;
-    uint64_t fsize = 0, coff = 0;  // next compressed byte to read
+    FileMap file;
+    uint64_t coff = 0;  // next block to scan
     int nthreads = 1;
     std::vector<std::string> names;
     std::vector<int64_t> lens;
-    std::vector<uint8_t> cbuf;  // compressed bytes read but not inflated (a block's start first)
-    uvec<uint8_t> pend;         // inflated bytes; [pbeg, pend.size()) not handed out yet
+    std::unique_ptr<MapBuf> pend;  // inflated bytes (anonymous mapping: no zero fill)
+    uint64_t pend_n = 0;           // bytes used in pend; [pbeg, pend_n) not handed out yet
     uint64_t pbeg = 0;
+    Hop hop;  // the next batch's records counted so far (offsets from pbeg)
+    uint64_t dropped = 0;  // mapping bytes already given back
+    double rec_bytes = 0.0;  // mean inflated bytes per record so far
     int64_t returned = 0;
-    ~bcio_stream() {
-        if (fd >= 0) ::close(fd);
-    }
-    bool all_read() const { return coff >= fsize && cbuf.empty(); }
+    bool all_read() const { return coff >= file.size(); }
+    const uint8_t* base() const { return pend ? pend->data() + pbeg : nullptr; }
+    uint64_t avail() const { return pend_n - pbeg; }
 };
 
 namespace {
 
-constexpr uint64_t kSlab = 16ull << 20;  // compressed bytes per read
-
-// read the next compressed slab and inflate its complete blocks onto pend; BCIO_OK, or an error
-// (a block cut off by the end of the file is the whole-file decoder's truncation error)
-int stream_fill(bcio_stream* s) {
-    if (s->coff < s->fsize) {
-        const uint64_t want = std::min<uint64_t>(kSlab, s->fsize - s->coff);
-        const size_t old = s->cbuf.size();
-        s->cbuf.resize(old + want);
-        uint64_t got = 0;
-        while (got < want) {
-            ssize_t r = ::pread(s->fd, s->cbuf.data() + old + got, want - got, (off_t)(s->coff + got));
-            if (r <= 0) return fail(BCIO_E_IO, "short read");
-            got += (uint64_t)r;
-        }
-        s->coff += want;
-    }
+// scan + inflate blocks from coff until they hold >= want inflated bytes (or the file ends)
+int stream_fill(bcio_stream* s, uint64_t want) {
+    const uint8_t* comp = s->file.data();
+    const uint64_t n = s->file.size();
     std::vector<Block> blocks;
-    uint64_t off = 0, uoff = 0;
-    const uint64_t n = s->cbuf.size();
-    while (off < n) {
+    uint64_t off = s->coff, uoff = 0;
+    while (off < n && uoff < want) {
         Block b;
         uint64_t bsize = 0;
-        int rc = scan_block(s->cbuf.data() + off, n - off, &b, &bsize);
-        if (rc == 1) {
-            if (s->coff >= s->fsize) return fail(BCIO_E_FORMAT, g_err);  // nothing more will come
-            break;
-        }
+        int rc = scan_block(comp + off, n - off, &b, &bsize);
+        if (rc == 1) return fail(BCIO_E_FORMAT, g_err);  // a block cut off by the end of the file
         if (rc != BCIO_OK) return rc;
         b.coff += off;
         b.uoff = uoff;
@@ -809,19 +820,27 @@ int stream_fill(bcio_stream* s) {
         blocks.push_back(b);
         off += bsize;
     }
-    // drop what was handed out before growing
-    if (s->pbeg > 0) {
-        const uint64_t keep = s->pend.size() - s->pbeg;
-        std::memmove(s->pend.data(), s->pend.data() + s->pbeg, keep);
-        s->pend.resize(keep);
-        s->pbeg = 0;
+    // one buffer: the bytes not handed out yet, then the new blocks' bytes
+    const uint64_t keep = s->avail();
+    auto next = std::make_unique<MapBuf>(keep + uoff + 64);
+    if (!next->ok()) return fail(BCIO_E_IO, "cannot allocate the inflate buffer");
+    if (keep) std::memcpy(next->data(), s->base(), keep);
+    if (!inflate_blocks(comp, blocks, next->data() + keep, s->nthreads)) return fail(BCIO_E_ZLIB, "inflate failed");
+    s->pend = std::move(next);
+    s->pend_n = keep + uoff;
+    s->pbeg = 0;
+    s->coff = off;
+    // give the consumed compressed pages back (whole pages below the next block)
+    const uint64_t page = 4096, upto = off / page * page;
+    if (upto > s->dropped) {
+        s->file.drop(s->dropped, upto - s->dropped);
+        s->dropped = upto;
     }
-    const uint64_t base = s->pend.size();
-    s->pend.resize(base + uoff);
-    if (!inflate_blocks(s->cbuf.data(), blocks, s->pend.data() + base, s->nthreads))
-        return fail(BCIO_E_ZLIB, "inflate failed");
-    s->cbuf.erase(s->cbuf.begin(), s->cbuf.begin() + (std::ptrdiff_t)off);
     return BCIO_OK;
+}
+
+void hop_reset(Hop& h) {
+    h = Hop();
 }
 
 }  // namespace
@@ -829,24 +848,23 @@ int stream_fill(bcio_stream* s) {
 extern "C" int bcio_stream_open(const char* path, int nthreads, bcio_stream** out) {
     if (!path || !out) return fail(BCIO_E_ARG, "null argument");
     *out = nullptr;
-    int fd = ::open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) return fail(BCIO_E_IO, std::string("cannot open ") + path);
     auto s = std::make_unique<bcio_stream>();
-    s->fd = fd;
-    struct stat st;
-    if (fstat(fd, &st) != 0) return fail(BCIO_E_IO, std::string("cannot stat ") + path);
-    s->fsize = (uint64_t)st.st_size;
+    int orc = s->file.open(path, /*sequential=*/true);
+    if (orc == -1) return fail(BCIO_E_IO, std::string("cannot open ") + path);
+    if (orc != 0) return fail(BCIO_E_IO, "short read");
     s->nthreads = hw_threads(nthreads);
-    for (;;) {  // the header, however many slabs it takes
+    uint64_t want = 4u << 20;
+    for (;;) {  // the header, however many blocks it takes
         uint64_t q = 0;
-        int rc = parse_header(s->pend.data(), s->pend.size(), s->names, s->lens, &q);
+        int rc = parse_header(s->base(), s->avail(), s->names, s->lens, &q);
         if (rc == BCIO_OK) {
-            s->pbeg = q;
+            s->pbeg += q;
             break;
         }
         if (rc < 0) return rc;
         if (s->all_read()) return fail(BCIO_E_FORMAT, g_err);
-        if ((rc = stream_fill(s.get())) != BCIO_OK) return rc;
+        if ((rc = stream_fill(s.get(), want)) != BCIO_OK) return rc;
+        want *= 2;
     }
     *out = s.release();
     return BCIO_OK;
@@ -855,45 +873,38 @@ extern "C" int bcio_stream_open(const char* path, int nthreads, bcio_stream** ou
 extern "C" int bcio_stream_next(bcio_stream* s, int64_t max_records, bcio_file** out) {
     if (!s || !out || max_records <= 0) return fail(BCIO_E_ARG, "bad argument");
     *out = nullptr;
-    // enough inflated bytes for max_records complete records, or the end of the file
-    uint64_t q_end = s->pbeg;
+    // the hop over the next batch's records, continued after each fill (each byte hopped once)
+    Hop& h = s->hop;
     for (;;) {
-        // count complete records without decoding (the hop of decode_records, no outputs)
-        int64_t m = 0;
-        uint64_t q = s->pbeg;
-        const uint64_t N = s->pend.size();
-        const uint8_t* p = s->pend.data();
-        while (q + 4 <= N && m < max_records) {
-            const uint32_t bs = rd32(p + q);
-            if (bs < 32) return fail(BCIO_E_FORMAT, "truncated BAM record");
-            if (q + 4 + bs > N) break;
-            q += 4 + (uint64_t)bs;
-            ++m;
-        }
-        if (m >= max_records || s->all_read()) {
-            q_end = q;
-            break;
-        }
-        int rc = stream_fill(s);
+        int rc = hop_records(h, s->base(), s->avail(), max_records, /*partial_ok=*/true);
         if (rc != BCIO_OK) return rc;
+        const int64_t m = (int64_t)h.starts.size();
+        if (m >= max_records || s->all_read()) break;
+        // the bytes the missing records should take (mean record size so far), at least 8 MiB
+        const double per = m > 0 ? (double)h.q / (double)m : (s->rec_bytes > 0 ? s->rec_bytes : 512.0);
+        const double need = per * (double)(max_records - m) * 1.05 + 65536.0;
+        const uint64_t want = (uint64_t)std::min(std::max(need, 8.0 * (1 << 20)), 8.0 * (1ull << 30));
+        if ((rc = stream_fill(s, want)) != BCIO_OK) return rc;
     }
-    if (q_end == s->pbeg) {
-        if (s->pbeg < s->pend.size()) {  // bytes left that never make a whole record
-            return fail(BCIO_E_FORMAT, s->pend.size() - s->pbeg < 4 ? "truncated record length" : "truncated BAM record");
-        }
+    if (h.starts.empty()) {
+        if (s->avail())  // bytes left that never make a whole record
+            return fail(BCIO_E_FORMAT, s->avail() < 4 ? "truncated record length" : "truncated BAM record");
         return BCIO_OK;  // end of file
     }
     auto* f = new bcio_file();
     f->names = s->names;
     f->lens = s->lens;
-    uint64_t q_dec = s->pbeg;
-    int rc = decode_records(f, s->pend.data(), s->pbeg, q_end, max_records, false, s->nthreads, &q_dec, nullptr);
+    const uint64_t used = h.q;
+    const int64_t got = (int64_t)h.starts.size();
+    int rc = fill_records(f, s->base(), h, s->nthreads, nullptr);
+    hop_reset(h);
     if (rc != BCIO_OK) {
         delete f;
         return rc;
     }
-    s->pbeg = q_dec;
-    s->returned += (int64_t)f->tid.size();
+    s->rec_bytes = (double)used / (double)got;
+    s->pbeg += used;
+    s->returned += got;
     *out = f;
     return BCIO_OK;
 }

@@ -543,13 +543,29 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     extra_us = {}
     if "rc" in launched and not summarise:  # deep: k_rc + k_stats (bc_count: k_rc alone)
         kern_s["rc"] = region(wl.count_only, reps)
-        kern_s["stats"] = region(wl.stats_only, reps)
         # what the step does not pay for: k_rc from the raw batch (CIGAR words
         # decoded in the kernel), the device index build on its own, and whole steps from the
         # raw batch (index build + k_rc + k_stats)
         kern_s["rc_no_index"] = region(lambda: wl.count_only("no_index"), reps)
-        kern_s["index"] = region(wl.rebuild, reps)
-        extra_us["raw_step_us"] = region(wl.raw_step, reps) * 1e6
+        # short launches: their own durations from the library's per-launch events (a region of
+        # back-to-back Python calls would time the host's issue rate instead)
+        ctx.timing(True)
+        for _ in range(reps):
+            wl.stats_only()
+            wl.rebuild()
+        rep = ctx.timing_report()
+        ctx.timing(False)
+        kern_s["stats"] = rep["stats"][1] * 1e-6
+        kern_s["index"] = rep["index"][1] * 1e-6
+        # whole steps from the raw batch (index build + k_rc + k_stats), K of them in one graph
+        g = ctx.capture(lambda: [wl.raw_step() for _ in range(steps)])
+        g.launch()
+        ctx.sync()
+        ctx.event_record(2)
+        g.launch()
+        ctx.event_record(3)
+        extra_us["raw_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        del g
     gather_us = None
     if gather is not None:
         if group is not None:
@@ -692,7 +708,10 @@ def run_unsorted(ctx, args, reps: int = 20) -> dict:
 
     for _ in range(3):
         sorted_step()
-    ss_us = region(sorted_step, reps)
+    g = ctx.capture(lambda: [sorted_step() for _ in range(reps)])  # device time, not the host's issue rate
+    g.launch()
+    ss_us = region(g.launch, 1) / reps
+    del g
     ok_s = bool(np.array_equal(counts.download(np.int32, k * L).reshape(k, L), exp[:, :k].T.astype(np.int32)))
     for x in (counts, cov, pc, ent, sec, mem, imem):
         x.free()

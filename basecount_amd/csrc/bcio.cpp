@@ -917,7 +917,15 @@ extern "C" const char* bcio_stream_ref_name(const bcio_stream* s, int32_t i) {
 extern "C" int64_t bcio_stream_ref_len(const bcio_stream* s, int32_t i) {
     return (s && i >= 0 && i < (int32_t)s->lens.size()) ? s->lens[i] : -1;
 }
-extern "C" void bcio_stream_close(bcio_stream* s) { delete s; }
+// like bcio_close: unmapping a batch-sized buffer takes ms, nothing waits for it
+extern "C" void bcio_stream_close(bcio_stream* s) {
+    if (!s) return;
+    try {
+        std::thread([s] { delete s; }).detach();
+    } catch (...) {
+        delete s;
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // writer

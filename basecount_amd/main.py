@@ -208,6 +208,26 @@ class _Scratch:
         self.bufs.clear()
 
 
+_SCRATCHES: dict = {}
+
+
+def _scratch(ctx) -> _Scratch:
+    """The device's grow-only scratch, kept from call to call (a hipFree synchronises and costs
+    ~2 ms each: releasing a call's dozen buffers cost more than its kernels); give the HBM back
+    with release_device_memory()."""
+    sc = _SCRATCHES.get(ctx.device)
+    if sc is None or sc.ctx is not ctx:
+        sc = _SCRATCHES[ctx.device] = _Scratch(ctx)
+    return sc
+
+
+def release_device_memory() -> None:
+    """Free the HBM the CLI / library calls keep for reuse (batch buffers, outputs)."""
+    for sc in _SCRATCHES.values():
+        sc.release()
+    _SCRATCHES.clear()
+
+
 def _download(outs, counts, k, L) -> RefData:
     cov = outs["cov"].download(np.int32, L)
     ent = outs["ent"].download(np.float64, L)
@@ -509,7 +529,7 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         acc = {}  # ref -> device histogram accumulating its batches (int32 [ncols][L])
         finished = set()
         ctx = context(device) if (mbq_ok and mine) else None
-        scratch = _Scratch(ctx) if ctx is not None else None
+        scratch = _scratch(ctx) if ctx is not None else None
         nf, nf2 = norm_factors(k)
 
         def tiles_of(ref):
@@ -600,8 +620,6 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 ctx.sync()
             for b in acc.values():
                 b.free()
-            if scratch is not None:
-                scratch.release()
         if _group is not None and mbq_ok:
             # every rank needs every reference's first out-of-range read to raise the same error
             flat = [v for r in ref_order for v in fl.range_.get(r, (-2, -1))]

@@ -19,7 +19,7 @@ namespace {
 
 #include "bc_walk.h"
 
-constexpr int kCigStage = 4096;  // CIGAR words a k_index_runs block stages (16 KiB)
+constexpr int kCigStage = 2048;  // CIGAR words a k_index_runs block stages (8 KiB: 8 per read)
 
 struct IdxArgs {
     const int32_t* pos;
@@ -67,8 +67,12 @@ __global__ __launch_bounds__(kRcChunkReads) void k_index_runs(IdxArgs A) {
 #pragma unroll
     for (int k = 0; k < kPre; ++k)
         w[k] = (valid && (uint32_t)k < cn) ? (mine_in ? cig[cb - s0 + k] : A.cigar[cb + k]) : 0u;
+    // ops decoded: the wave's longest CIGAR (up to kPre; the decode's per-op select chain is
+    // the kernel's VALU cost, and most waves' reads have far fewer ops)
+    const int cmax = (int)(uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)wave_reduce<true>(valid ? (cn < (uint32_t)kPre ? cn : (uint32_t)kPre) : 0u));
     uint32_t q[4];
-    pack_runs(decode_runs<2>(w, cn, kPre), q);
+    pack_runs(decode_runs<2>(w, cn, cmax), q);
     if (valid) A.runs[i] = make_uint4(q[0], q[1], q[2], q[3]);
     if (!A.sums) return;  // (uniform)
     // the summary from the record, as the kernel will read it (pack_runs may mark a read complex)

@@ -9,10 +9,12 @@
 //                      (the returned old value is the read's rank inside the bin), and the
 //                      read's query length from its CIGAR (M/I/=/X);
 //   2. scan_u32        exclusive prefix sum of the bins (3 launches: tile sums, their scan, add);
-//   3. k_sort_scatter  each read's fields to its sorted slot, with the bytes of sequence it needs;
+//   3. k_sort_perm     the permutation (one random 4-byte store per read), then k_sort_gather:
+//                      each sorted slot's fields gathered with coalesced stores, and the bytes of
+//                      sequence it needs (rounded up to whole words);
 //   4. scan_u32        of those bytes: the sorted sequence buffer's offsets;
-//   5. k_sort_seq      each read's aligned sequence (and its qualities) copied to its offset, so
-//                      a chunk of sorted reads has one contiguous sequence segment again.
+//   5. k_sort_seq      each read's aligned sequence (and its qualities) copied word by word to its
+//                      offset, so a chunk of sorted reads has one contiguous sequence segment again.
 // The CIGAR buffer is shared with the input (reads keep their cig_beg).  HBM traffic ~ 2x the
 // batch's sequence + 40 B per read; every pass is a streaming, fully parallel kernel.
 #include "bc_internal.h"
@@ -126,6 +128,7 @@ struct SortArgs {
     uint32_t* rank;   // [n] rank of read i inside its bin
     uint32_t* qlen;   // [n] query bases of read i (M/I/=/X)
     uint32_t* src;    // [n] source nibble index of sorted read j
+    uint32_t* perm;   // [n] the read at sorted slot j
     int32_t* o_pos;
     uint32_t* o_cig_beg;
     uint32_t* o_cig_n;
@@ -136,6 +139,7 @@ struct SortArgs {
     uint8_t* o_seq;
     uint8_t* o_qual;
     uint32_t cap;       // bytes of o_seq (o_qual: twice as many)
+    int64_t qual_bytes;
 };
 
 __global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
@@ -151,20 +155,32 @@ __global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
     A.qlen[i] = q;
 }
 
-__global__ __launch_bounds__(256) void k_sort_scatter(SortArgs A) {
+// read i's sorted slot; only the permutation is written at random (one 4-byte store per read)
+__global__ __launch_bounds__(256) void k_sort_perm(SortArgs A) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= A.n) return;
-    const uint32_t j = A.bins[A.pos[i]] + A.rank[i];
+    A.perm[A.bins[A.pos[i]] + A.rank[i]] = (uint32_t)i;
+}
+
+// sorted read j = read perm[j]: its fields gathered (random reads, coalesced writes), with the
+// bytes of sequence it will take (a multiple of 4, so every output word belongs to one read)
+__global__ __launch_bounds__(256) void k_sort_gather(SortArgs A) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= A.n) return;
+    const uint32_t i = A.perm[j];
     const uint32_t sn = A.seq_nib[i];
     A.o_pos[j] = A.pos[i];
     A.o_cig_beg[j] = A.cig_beg[i];
     A.o_cig_n[j] = A.cig_n[i];
     A.src[j] = sn;
-    A.o_bytes[j] = ((sn & 1u) + A.qlen[i] + 1u) >> 1;  // the whole bytes holding its aligned bases
+    A.o_bytes[j] = (((sn & 1u) + A.qlen[i] + 1u) / 2u + 3u) & ~3u;
 }
 
-// 16 lanes per sorted read: its bytes of sequence (and the two quality bytes of each) copied to
-// its offset, lane-strided; the new nibble index keeps the old one's parity
+// 16 lanes per sorted read, one 4-byte word each: the read's bytes from its source offset
+// (any alignment: two aligned source words and a funnel shift) to its 4-aligned offset, and the
+// two quality bytes of each; the new nibble index keeps the old one's parity.  The source is
+// read up to 3 bytes past the read (the padded buffers allow it): those bytes land in the read's
+// own padding, which no kernel reads (every walk masks to the read's aligned bases).
 __global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
     const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
     const uint32_t sub = threadIdx.x & 15u;
@@ -175,15 +191,35 @@ __global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
         if (sub == 0) atomicOr(A.overflow, 1u);
         return;
     }
-    const uint32_t from = sn >> 1, len = end - off;
-    for (uint32_t k = sub; k < len; k += 16) A.o_seq[off + k] = A.seq[from + k];
-    if (A.qual)
-        for (uint32_t k = sub; k < 2 * len; k += 16) A.o_qual[2 * (uint64_t)off + k] = A.qual[2 * (uint64_t)from + k];
+    const uint32_t from = sn >> 1, words = (end - off) >> 2;
+    const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
+    const uint32_t sh = (from & 3u) * 8u;
+    uint32_t* d32 = (uint32_t*)(A.o_seq + off);
+    for (uint32_t w = sub; w < words; w += 16) d32[w] = __builtin_amdgcn_alignbit(s32[w + 1], s32[w], sh);
+    if (A.qual) {
+        const uint64_t qf = 2 * (uint64_t)from;
+        const uint32_t* q32 = (const uint32_t*)(A.qual + (qf & ~3ull));
+        const uint32_t qsh = (uint32_t)(qf & 3u) * 8u;
+        uint32_t* dq = (uint32_t*)(A.o_qual + 2 * (uint64_t)off);
+        const uint64_t q0 = qf & ~3ull;
+        for (uint32_t w = sub; w < 2 * words; w += 16) {
+            if (q0 + 4ull * w + 8 <= (uint64_t)A.qual_bytes) {
+                dq[w] = __builtin_amdgcn_alignbit(q32[w + 1], q32[w], qsh);
+            } else {  // the buffer's last bytes (the quality buffer has no padding)
+                uint32_t v = 0;
+                for (uint32_t bb = 0; bb < 4; ++bb) {
+                    const uint64_t at = qf + 4ull * w + bb;
+                    if (at < (uint64_t)A.qual_bytes) v |= (uint32_t)A.qual[at] << (8 * bb);
+                }
+                dq[w] = v;
+            }
+        }
+    }
     if (sub == 0) A.o_seq_nib[j] = 2 * off + (sn & 1u);
 }
 
 struct SortLayout {
-    size_t bins, rank, qlen, src, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, total;
+    size_t bins, rank, qlen, src, perm, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, total;
     int64_t nbins;
     uint32_t cap;
 };
@@ -192,7 +228,8 @@ SortLayout sort_layout(const bc_reads& r) {
     SortLayout L{};
     const int64_t n = r.n_reads;
     L.nbins = r.max_end + 2;  // every start <= max_end
-    L.cap = (uint32_t)std::min<int64_t>(r.seq_bytes + n + 16, 0xFFFFFFF0ll);
+    // every read takes its aligned bases' bytes rounded up to 4 (+ 1 for an odd start)
+    L.cap = (uint32_t)std::min<int64_t>(r.seq_bytes + 5 * n + 16, 0xFFFFFFF0ll);
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t at = off;
@@ -203,6 +240,7 @@ SortLayout sort_layout(const bc_reads& r) {
     L.rank = take(4 * (size_t)n);
     L.qlen = take(4 * (size_t)n);
     L.src = take(4 * (size_t)n);
+    L.perm = take(4 * (size_t)n);
     L.o_pos = take(4 * (size_t)n);
     L.o_cb = take(4 * (size_t)n);
     L.o_cn = take(4 * (size_t)n);
@@ -239,6 +277,7 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     A.rank = (uint32_t*)(b + L.rank);
     A.qlen = (uint32_t*)(b + L.qlen);
     A.src = (uint32_t*)(b + L.src);
+    A.perm = (uint32_t*)(b + L.perm);
     A.o_pos = (int32_t*)(b + L.o_pos);
     A.o_cig_beg = (uint32_t*)(b + L.o_cb);
     A.o_cig_n = (uint32_t*)(b + L.o_cn);
@@ -249,16 +288,18 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     A.o_seq = b + L.o_seq;
     A.o_qual = r.qual ? b + L.o_qual : nullptr;
     A.cap = L.cap;
+    A.qual_bytes = r.qual ? r.qual_bytes : 0;
     uint32_t* tmp = (uint32_t*)(b + L.tmp);
     const unsigned blocks = (unsigned)((r.n_reads + 255) / 256);
     hipError_t e = hipMemsetAsync(A.bins, 0, 4 * (size_t)L.nbins, s);
     if (e == hipSuccess) e = hipMemsetAsync(A.total, 0, 16, s);
-    // the sorted sequence's padding (BC_SEQ_EVENT) is zero
-    if (e == hipSuccess) e = hipMemsetAsync(A.o_seq, 0, seq_event_bytes(L.cap), s);
+    // the sorted sequence's padding past cap (BC_SEQ_EVENT) is zero
+    if (e == hipSuccess) e = hipMemsetAsync(A.o_seq + L.cap, 0, seq_event_bytes(L.cap) - L.cap, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sort_count, dim3(blocks), dim3(256), 0, s, A);
     if ((e = scan_u32(s, A.bins, L.nbins, tmp, nullptr)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sort_scatter, dim3(blocks), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_sort_perm, dim3(blocks), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_sort_gather, dim3(blocks), dim3(256), 0, s, A);
     if ((e = scan_u32(s, A.o_bytes, r.n_reads, tmp, A.total)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_sort_seq, dim3((unsigned)((r.n_reads * 16 + 255) / 256)), dim3(256), 0, s, A);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -325,6 +325,29 @@ class Workload:
             ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
                              [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
 
+    def pipelined(self, steps: int, side):
+        """K steps with two in flight: they alternate between the main context and ``side`` (each
+        with its own read-chunked scratch and output buffers), so a step's kernel 2 and the next
+        step's kernel 1 overlap, as consecutive batches of a stream would.  Enqueued (and
+        capturable) on the main context: fork, two chains of steps, join."""
+        main = self.ctx
+        if not hasattr(self, "_pipe_out"):
+            k = self.k
+            self._pipe_out = []
+            for _, L, _, _, o in self.work:
+                self._pipe_out.append(dict(counts=main.alloc(4 * k * L), cov=main.alloc(4 * L),
+                                           pc=main.alloc(8 * k * L) if self.want_pc else None,
+                                           ent=main.alloc(8 * L), sec=main.alloc(8 * L)))
+        side.wait(main)
+        for i in range(steps):
+            c = main if i % 2 == 0 else side
+            j = self._next()
+            for (_, L, _, reads, o), o2 in zip(self.work, self._pipe_out):
+                out = o if i % 2 == 0 else o2
+                c.pileup(reads[j], L, self.mbq, self.k, self.nf, self.nf2, out["counts"].ptr, out["cov"].ptr,
+                         out["pc"].ptr if out["pc"] is not None else None, out["ent"].ptr, out["sec"].ptr)
+        main.wait(side)
+
     def variant(self, name: str):
         """Per copy and contig, a bc_reads of the same device batch: "no_index" without its
         index (the kernels decode the CIGARs / search pos[] themselves), "rebuilt" whose index
@@ -427,6 +450,11 @@ class Workload:
             for v in o.values():
                 if v is not None:
                     v.free()
+        for o in getattr(self, "_pipe_out", []):
+            for v in o.values():
+                if v is not None:
+                    v.free()
+        self._pipe_out = []
         if self.d_sum is not None:
             self.d_sum.free()
         self.work = []
@@ -566,6 +594,25 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         ctx.event_record(3)
         extra_us["raw_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
         del g
+    if not summarise and group is None and len(wl.ctxs) == 1:
+        # two steps in flight on two streams (consecutive batches of a stream overlap): reported
+        # beside the serialized step, never as `value`
+        from basecount_amd import device as Dm
+
+        side = Dm.Context(ctx.device)
+        side.set_shape(args.shape, args.tile_waves)
+        wl.pipelined(4, side)  # first use: the side context's scratch is allocated outside the capture
+        ctx.sync()
+        side.sync()
+        g = ctx.capture(lambda: wl.pipelined(steps, side))
+        g.launch()
+        ctx.sync()
+        ctx.event_record(2)
+        g.launch()
+        ctx.event_record(3)
+        extra_us["pipelined_2_streams_us_per_step"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        del g
+        side.close()
     gather_us = None
     if gather is not None:
         if group is not None:

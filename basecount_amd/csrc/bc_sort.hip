@@ -6,8 +6,8 @@
 // sequence.  An unsorted batch (reads of one reference in any order) is therefore put in start
 // order here, with no host round trip:
 //   1. k_sort_count    counting sort by start position: one atomic per read on its position's bin
-//                      (the returned old value is the read's rank inside the bin), and the
-//                      read's query length from its CIGAR (M/I/=/X);
+//                      (the returned old value is the read's rank inside the bin), the read's
+//                      query length from its CIGAR (M/I/=/X), its fields packed in 32 bytes;
 //   2. scan_u32        exclusive prefix sum of the bins (3 launches: tile sums, their scan, add);
 //   3. k_sort_perm     the permutation (one random 4-byte store per read), then k_sort_gather:
 //                      each sorted slot's fields gathered with coalesced stores, and the bytes of
@@ -125,8 +125,7 @@ struct SortArgs {
     const uint8_t* qual;
     int64_t n;
     uint32_t* bins;   // [nbins] counts, then offsets
-    uint32_t* rank;   // [n] rank of read i inside its bin
-    uint32_t* qlen;   // [n] query bases of read i (M/I/=/X)
+    uint4* rec;       // [2n] read i: {pos, cig_beg, cig_n, seq_nib}, {qlen, rank in its bin, 0, 0}
     uint32_t* src;    // [n] source nibble index of sorted read j
     uint32_t* perm;   // [n] the read at sorted slot j
     int32_t* o_pos;
@@ -142,38 +141,46 @@ struct SortArgs {
     int64_t qual_bytes;
 };
 
+// read i: its rank inside its start's bin (one atomic on the bin), its query length from the
+// CIGAR (M/I/=/X), and its fields packed into one 32-byte record (written coalesced), so the
+// gather below reads one 32-byte record per read instead of five scattered 4-byte fields
 __global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= A.n) return;
-    A.rank[i] = atomicAdd(&A.bins[A.pos[i]], 1u);
-    const uint32_t* cg = A.cigar + A.cig_beg[i];
+    const int32_t pos = A.pos[i];
+    const uint32_t cb = A.cig_beg[i], cn = A.cig_n[i], sn = A.seq_nib[i];
+    const uint32_t rank = atomicAdd(&A.bins[pos], 1u);
+    const uint32_t* cg = A.cigar + cb;
     uint32_t q = 0;
-    for (uint32_t k = 0, cn = A.cig_n[i]; k < cn; ++k) {
+    for (uint32_t k = 0; k < cn; ++k) {
         const uint32_t w = cg[k];
         if (qcons(w & 15u)) q += w >> 4;
     }
-    A.qlen[i] = q;
+    A.rec[2 * i] = make_uint4((uint32_t)pos, cb, cn, sn);
+    A.rec[2 * i + 1] = make_uint4(q, rank, 0u, 0u);
 }
 
 // read i's sorted slot; only the permutation is written at random (one 4-byte store per read)
 __global__ __launch_bounds__(256) void k_sort_perm(SortArgs A) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= A.n) return;
-    A.perm[A.bins[A.pos[i]] + A.rank[i]] = (uint32_t)i;
+    const uint4 a = A.rec[2 * i], b = A.rec[2 * i + 1];
+    A.perm[A.bins[a.x] + b.y] = (uint32_t)i;
 }
 
-// sorted read j = read perm[j]: its fields gathered (random reads, coalesced writes), with the
-// bytes of sequence it will take (a multiple of 4, so every output word belongs to one read)
+// sorted read j = read perm[j]: its record gathered (one random 32-byte read), its fields
+// written coalesced, with the bytes of sequence it will take (a multiple of 4, so every output
+// word belongs to one read)
 __global__ __launch_bounds__(256) void k_sort_gather(SortArgs A) {
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= A.n) return;
     const uint32_t i = A.perm[j];
-    const uint32_t sn = A.seq_nib[i];
-    A.o_pos[j] = A.pos[i];
-    A.o_cig_beg[j] = A.cig_beg[i];
-    A.o_cig_n[j] = A.cig_n[i];
-    A.src[j] = sn;
-    A.o_bytes[j] = (((sn & 1u) + A.qlen[i] + 1u) / 2u + 3u) & ~3u;
+    const uint4 a = A.rec[2 * (size_t)i], b = A.rec[2 * (size_t)i + 1];
+    A.o_pos[j] = (int32_t)a.x;
+    A.o_cig_beg[j] = a.y;
+    A.o_cig_n[j] = a.z;
+    A.src[j] = a.w;
+    A.o_bytes[j] = (((a.w & 1u) + b.x + 1u) / 2u + 3u) & ~3u;
 }
 
 // 16 lanes per sorted read, one 4-byte word each: the read's bytes from its source offset
@@ -219,7 +226,7 @@ __global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
 }
 
 struct SortLayout {
-    size_t bins, rank, qlen, src, perm, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, total;
+    size_t bins, rec, src, perm, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, total;
     int64_t nbins;
     uint32_t cap;
 };
@@ -237,8 +244,7 @@ SortLayout sort_layout(const bc_reads& r) {
         return at;
     };
     L.bins = take(4 * (size_t)L.nbins);
-    L.rank = take(4 * (size_t)n);
-    L.qlen = take(4 * (size_t)n);
+    L.rec = take(32 * (size_t)n);
     L.src = take(4 * (size_t)n);
     L.perm = take(4 * (size_t)n);
     L.o_pos = take(4 * (size_t)n);
@@ -274,8 +280,7 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     A.qual = r.qual;
     A.n = r.n_reads;
     A.bins = (uint32_t*)(b + L.bins);
-    A.rank = (uint32_t*)(b + L.rank);
-    A.qlen = (uint32_t*)(b + L.qlen);
+    A.rec = (uint4*)(b + L.rec);
     A.src = (uint32_t*)(b + L.src);
     A.perm = (uint32_t*)(b + L.perm);
     A.o_pos = (int32_t*)(b + L.o_pos);

@@ -657,15 +657,16 @@ def _no_reads() -> D.BcReads:
 
 def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
     """The slice as the fast kernels take it: an unsorted slice is first put in start order on
-    the device (bc_reads_sort, into the reusable scratch), then the device index the kernels
-    would use (bc_reads_index, BC_INDEX_AUTO: run records + chunk summaries for the read-chunked
-    kernel, the tile index for the tiled one), stream-ordered before the kernels."""
+    the device (bc_reads_sort, into the reusable scratch), then the tiled kernel's tile index
+    (bc_reads_index), stream-ordered before the kernels."""
     if not reads.sorted and reads.n_reads > 1:
         nb = ctx.sort_bytes(reads)
         reads = ctx.sort(reads, scratch.get("sorted", nb).ptr, nb)
-    nb = ctx.index_bytes(reads, L)
+    # the tile index only: a batch counted once does not recover the run records' build (C3:
+    # k_index_runs ~18 us against ~10 us saved in k_rc; bench.py reports both)
+    nb = ctx.index_bytes(reads, L, D.BC_INDEX_TILES)
     if nb:
-        ctx.index(reads, L, scratch.get("index", nb).ptr, nb)
+        ctx.index(reads, L, scratch.get("index", nb).ptr, nb, D.BC_INDEX_TILES)
     return reads
 
 

@@ -989,6 +989,8 @@ def main():
         }
         if "gather_us" in head:
             line["gather_us"] = head["gather_us"]
+        if "pipelined_2_streams_us_per_step" in head:
+            line["pipelined_2_streams_us_per_step"] = head["pipelined_2_streams_us_per_step"]
         if cpu:
             line["speedup_vs_cpu"] = head["value"] / cpu["value"]
             line["speedup_vs_cpu_all_cores"] = head["value"] / cpu_all["value"]

@@ -104,3 +104,23 @@ def test_cli_rccl_world1_matches_golden(tmp_path):
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     with gzip.open(os.path.join(GOLD, man["stdout"])) as fh:
         assert p.stdout == fh.read()
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_rehearsal():
+    """`bench.py --gpus 2` as the driver runs it (no launcher: the script starts its two ranks),
+    both ranks on the box's one GPU with the exchange over gloo (RCCL refuses two ranks on one
+    GPU): one JSON line from rank 0 with n_gpus 2, the C5 strong-scaling extra gathered from
+    both ranks, parity true."""
+    env = dict(os.environ, BASECOUNT_DIST_BACKEND="gloo")
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5",
+                        "--warmup", "2"], env=env, capture_output=True, timeout=600, cwd=REPO)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    lines = [ln for ln in p.stdout.decode().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["comm"] == "gloo" and d["parity_vs_oracle"]
+    c5 = d["extra"]["c5"]
+    assert c5["parity_vs_oracle"] and c5["gather_bytes"] == 32 * 24 and c5["scaling"] == "strong"

@@ -208,6 +208,27 @@ class _Scratch:
         self.bufs.clear()
 
 
+# host phases of get_basecounts (seconds), accumulated; printed by BASECOUNT_HIP_TIMING=1
+PHASES: dict = {}
+
+
+class _phase:
+    __slots__ = ("name", "t0")
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        import time
+
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        import time
+
+        PHASES[self.name] = PHASES.get(self.name, 0.0) + time.perf_counter() - self.t0
+
+
 _SCRATCHES: dict = {}
 
 
@@ -538,11 +559,13 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         base = 0  # accepted reads before the current batch (global ordinals)
         cur = nxt = None
         try:
-            cur = stream.next_batch(B)
+            with _phase("decode"):
+                cur = stream.next_batch(B)
             sel_next = None
             while cur is not None:
                 f = cur
-                sel = sel_next if sel_next is not None else f.select(mmq, wanted)
+                with _phase("select"):
+                    sel = sel_next if sel_next is not None else f.select(mmq, wanted)
                 sel_next = None
                 fl.n_records += f.n_records
                 # in-loop faults (global ordinals); type faults per reference
@@ -567,12 +590,17 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                         here.append(ref)
                 # one batch of look-ahead: a reference absent from the next batch is complete
                 # (in a file grouped by reference); none after the reference's first in-loop fault
-                nxt = stream.next_batch(B) if fl.inloop() is None else None
+                with _phase("decode"):
+                    nxt = stream.next_batch(B) if fl.inloop() is None else None
                 if ctx is not None and here:
                     if any(r in finished for r in here):
                         raise _Ungrouped()
-                    nsel = sel_next = nxt.select(mmq, wanted) if (nxt is not None and grouped) else None
-                    bod = _BatchOnDevice(ctx, f, sel, need_qual=mbq > 0, scratch=scratch)
+                    with _phase("select"):
+                        nsel = sel_next = nxt.select(mmq, wanted) if (nxt is not None and grouped) else None
+                    with _phase("upload"):
+                        bod = _BatchOnDevice(ctx, f, sel, need_qual=mbq > 0, scratch=scratch)
+                    t_refs = _phase("kernels + download")
+                    t_refs.__enter__()
                     for ref in here:
                         t = ref_index[ref]
                         L = int(reference_lengths[ref])
@@ -597,7 +625,9 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                         if bad >= 0 and ref not in fl.range_:
                             fl.range_[ref] = (base + int(sel.ordinal[b0 + bad]),
                                               _bad_pos(f, int(sel.rec[b0 + bad]), mbq, L))
-                    ctx.sync()  # the batch's host arrays may go once its copies are done
+                    t_refs.__exit__()
+                    with _phase("device (sync)"):
+                        ctx.sync()  # the batch's host arrays may go once its copies are done
                 base += sel.n_accepted
                 cur.close()
                 cur, nxt = nxt, None
@@ -972,6 +1002,8 @@ def _timing_report(wall_s: float) -> None:
     for name, v in sorted(rep.items()):
         if isinstance(v, tuple):
             print(f"basecount[{rank}] kernel {name}: {v[0]} launches, {v[1]:.2f} us mean", file=sys.stderr)
+    for name, v in PHASES.items():
+        print(f"basecount[{rank}] host {name}: {v * 1e3:.2f} ms", file=sys.stderr)
     print(f"basecount[{rank}] wall {wall_s * 1e3:.2f} ms", file=sys.stderr)
 
 
@@ -985,11 +1017,12 @@ def _run(args, references, min_base_quality, min_mapping_quality, chunk_size, be
         if group is None:
             bc = BaseCount(args.bam, **kw)
             print("\t".join(bc.columns))
-            for ref in bc.references:
-                rows = bc.data[ref]["rows"]
-                d = rows.d
-                fmt.write_bytes(fmt.rows_text(ref, d.counts[: rows.k], d.pc, d.ent, d.sec, dp,
-                                              rows.long))
+            with _phase("format + write"):
+                for ref in bc.references:
+                    rows = bc.data[ref]["rows"]
+                    d = rows.d
+                    fmt.write_bytes(fmt.rows_text(ref, d.counts[: rows.k], d.pc, d.ent, d.sec, dp,
+                                                  rows.long))
             return
         out, owner, order = get_basecounts(args.bam, **kw, _group=group)
         if group.rank == 0:

@@ -574,17 +574,20 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         # what the step does not pay for: k_rc from the raw batch (CIGAR words
         # decoded in the kernel), the device index build on its own, and whole steps from the
         # raw batch (index build + k_rc + k_stats)
-        kern_s["rc_no_index"] = region(lambda: wl.count_only("no_index"), reps)
         # short launches: their own durations from the library's per-launch events (a region of
         # back-to-back Python calls would time the host's issue rate instead)
         ctx.timing(True)
         for _ in range(reps):
             wl.stats_only()
-            wl.rebuild()
+            if not args.lean:
+                wl.rebuild()
         rep = ctx.timing_report()
         ctx.timing(False)
         kern_s["stats"] = rep["stats"][1] * 1e-6
-        kern_s["index"] = rep["index"][1] * 1e-6
+        if "index" in rep:
+            kern_s["index"] = rep["index"][1] * 1e-6
+    if "rc" in launched and not summarise and not args.lean:
+        kern_s["rc_no_index"] = region(lambda: wl.count_only("no_index"), reps)
         # whole steps from the raw batch (index build + k_rc + k_stats), K of them in one graph
         g = ctx.capture(lambda: [wl.raw_step() for _ in range(steps)])
         g.launch()
@@ -594,7 +597,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         ctx.event_record(3)
         extra_us["raw_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
         del g
-    if not summarise and group is None and len(wl.ctxs) == 1:
+    if not summarise and group is None and len(wl.ctxs) == 1 and not args.lean:
         # two steps in flight on two streams (consecutive batches of a stream overlap): reported
         # beside the serialized step, never as `value`
         from basecount_amd import device as Dm
@@ -686,10 +689,10 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                      "algorithmic_bytes": kbytes},
     }
     res.update(extra_us)
-    if "rc" in kern_s:
+    if "rc_no_index" in kern_s:
         nb = wl.bytes_dominant("rc")
         res["rc_frac_without_index"] = nb / kern_s["rc_no_index"] / 1e9 / HBM_PEAK_GBS
-        res["index_us"] = kern_s["index"] * 1e6
+        res["index_us"] = kern_s.get("index", 0.0) * 1e6
     if gather_us is not None:
         res["gather_us"] = gather_us
         res["gather_bytes"] = int(gather[0].sum())
@@ -867,6 +870,9 @@ def main():
                          "would otherwise stay in the 256 MB Infinity Cache, else 1)")
     ap.add_argument("--tile-index", choices=["on", "off"], default="on",
                     help="off: drop the upload's per-tile read ranges (bc_reads.tile_reads), A/B only")
+    ap.add_argument("--lean", action="store_true",
+                    help="time the step's own kernels only (no index / no-index / pipelined variants): "
+                         "every dispatch of the dominant kernel is then the measured kind (PMC passes)")
     ap.add_argument("--allow-diag", action="store_true",
                     help="run a diagnostic (BC_DIAG) build; its numbers are marked as such")
     args = ap.parse_args()

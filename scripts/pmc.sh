@@ -10,6 +10,6 @@ sets=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_C
       "FETCH_SIZE" "WRITE_SIZE")
 for i in ${PASSES:-1 2 3 4 5}; do
   set=${sets[$((i-1))]}
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/p$i -o run -- python bench.py --no-cpu-baseline --no-extras --no-e2e --launch eager --steps 20 --warmup 2 ${BENCH_ARGS} > $OUT/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/p$i -o run -- python bench.py --no-cpu-baseline --no-extras --no-e2e --lean --launch eager --steps 20 --warmup 2 ${BENCH_ARGS} > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; case $rc in 124|134|137|139) exit $rc;; esac
 done

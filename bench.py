@@ -905,7 +905,13 @@ def main():
     if world > 1:
         from basecount_amd.dist import Group
 
-        group = Group(ctx=ctx)  # RCCL over xGMI (BASECOUNT_DIST_BACKEND=gloo: rehearsal)
+        try:
+            group = Group(ctx=ctx)  # RCCL over xGMI (BASECOUNT_DIST_BACKEND=gloo: rehearsal)
+        except Exception as e:  # noqa: BLE001 - the curve is still measurable over gloo: say so
+            print(f"bench.py rank {rank}: RCCL group failed ({e}); falling back to gloo", file=sys.stderr,
+                  flush=True)
+            group = Group("gloo")
+            group.fallback = f"rccl failed: {e}"
 
     head = run_config(args.config, ctx, group, args, rank, world, args.steps, args.warmup, args.launch,
                       summarise=(args.config == "c5"))
@@ -977,6 +983,7 @@ def main():
                        "percentages_stored": args.config != "c5",
                        "parallelism": f"contig-sharded x{world}",
                        "comm": (group.backend if group is not None else None),
+                       "comm_fallback": getattr(group, "fallback", None),
                        "shape": args.shape, "tile_waves": args.tile_waves,
                        "summary_path": args.summary_path, "tile_index": args.tile_index,
                        "read_runs": args.read_runs, "build": build, "lib_sha16": lib_sha16()},

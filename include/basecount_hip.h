@@ -85,14 +85,16 @@ typedef struct bc_reads {
     /* Optional device index of a sorted batch (NULL / 0: the tiled kernel searches pos[]).  For
      * the 64-position tile t < n_tiles, tile_reads[2t] and tile_reads[2t+1] are the reads
      * [lo, hi) that can overlap it: lo = first i with pos[i] > 64t - max_span, hi = first i with
-     * pos[i] >= 64t + 64 (so valid for this max_span only).  bc_reads_upload builds it for dense
-     * batches (fewer tiles than reads/16, fewer than 2^31 reads); host inputs ignore it.       */
+     * pos[i] >= 64t + 64 (so valid for this max_span only).  Built on the device by
+     * bc_reads_upload / bc_reads_index (k_index_tiles) for dense batches (fewer tiles than
+     * reads/16, fewer than 2^31 reads); host inputs ignore it.                                  */
     const int32_t* tile_reads;
     int64_t n_tiles;
     /* Optional device run records of a sorted batch (NULL: the kernels decode the CIGARs): 4
      * words per read, the first two aligned runs of its CIGAR as the read-chunked kernel needs
-     * them (layout in basecount_amd/csrc/bc_runs.h).  bc_reads_upload decodes every read once
-     * on the host (the same decode the kernels run) for sorted batches; host inputs ignore it.
+     * them (layout in basecount_amd/csrc/bc_runs.h).  Built on the device by bc_reads_upload /
+     * bc_reads_index (k_index_runs: the same decode the kernels run) for sorted batches that
+     * take the read-chunked kernel; host inputs ignore it.
      * When run_chunks > 0, read_runs[4 n_reads ..] then holds run_chunks summaries of 8 words,
      * one per 256 consecutive reads (the read-chunked kernel's chunk): min start, max end,
      * first / last-plus-one byte of their aligned sequence, max span, a run-shape code and a

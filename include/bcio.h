@@ -107,9 +107,10 @@ int bcio_select(bcio_file* f, int64_t min_mapq, const uint8_t* ref_sel, bcio_sel
  * (file order) into a new bcio_file handle — bcio_get_records / bcio_select work on it as on a
  * whole file, its record indices and ordinals counting from the batch's first record — which the
  * caller releases with bcio_close.  *out = NULL at the end of the file.  Live memory is one
- * batch plus a compressed slab and its inflated bytes (the file is read with pread, never
- * mapped whole).  bcio_stream_records: records handed out so far (the next batch's first
- * record index in the file).                                                                  */
+ * batch plus the inflated bytes it was cut from: the file is mapped read-only, each fill
+ * inflates just the blocks the batch is estimated to need in one parallel pass, and the pages
+ * of consumed compressed blocks are given back (MADV_DONTNEED).  bcio_stream_records: records
+ * handed out so far (the next batch's first record index in the file).                       */
 typedef struct bcio_stream bcio_stream;
 int bcio_stream_open(const char* path, int nthreads, bcio_stream** out);
 int bcio_stream_next(bcio_stream* s, int64_t max_records, bcio_file** out);

@@ -2,9 +2,10 @@
 (no config may stay untested on the GPU).
 
   C5  24 GRCh38-sized contigs (3.09 Gb) x 50,000 reads: every contig through bc_pileup +
-      bc_summary (the sparse k_pileup_solo shape), coverage sums == events piled on all 24,
-      counts exact and entropies bit-identical on chr21, chr22, chrY and chr1 (249 Mb); then the
-      CLI's --summarise over a written BAM == the oracle's main.py:469-499 text for all 24.
+      bc_summary (the sparse k_pileup_solo shape), one test per contig: coverage sum == events
+      piled, counts exact and coverage / entropies / secondary entropies bit-identical to the
+      oracle at every position of all 24 (3.09 G positions); then the CLI's --summarise over a
+      written BAM == the oracle's main.py:469-499 text for all 24.
   C4  1,000,000 mixed-CIGAR reads + the 98-amplicon BED through the CLI's --summarise-with-bed
       (the deep k_rc -> k_stats -> k_sum -> k_amplicon chain) == main.py:469-595 from the oracle.
   C3  the same reads through the CLI's default per-position rows == main.py:454-466 from the
@@ -49,45 +50,48 @@ def c5():
     return synth.make_config("c5")
 
 
-def test_c5_every_contig(ctx, c5):
+@pytest.fixture(scope="module")
+def c5_event(c5):
+    return seq_to_event(c5.seq)
+
+
+@pytest.mark.parametrize("t", range(len(synth.GRCH38)), ids=[n for n, _ in synth.GRCH38])
+def test_c5_contig(ctx, c5, c5_event, t):
     rs = c5
-    ev = seq_to_event(rs.seq)
     k = 5
     nf, nf2 = norm_factors(k)
-    full = {"chr21", "chr22", "chrY", "chr1"}
-    for t, (name, L) in enumerate(zip(rs.references, rs.lengths)):
-        b = synth.batch_arrays(rs, t, 0)
-        r = D.DeviceReads(ctx, dict(b, seq_event=ev))
-        bufs = [ctx.alloc(n) for n in (4 * k * L, 4 * L, 8 * L, 8 * L, D.summary_work_bytes(L), 32)]
-        counts, cov, ent, sec, work, out = bufs
+    name, L = rs.references[t], rs.lengths[t]
+    b = synth.batch_arrays(rs, t, 0)
+    r = D.DeviceReads(ctx, dict(b, seq_event=c5_event))
+    bufs = [ctx.alloc(n) for n in (4 * k * L, 4 * L, 8 * L, 8 * L, D.summary_work_bytes(L), 32)]
+    counts, cov, ent, sec, work, out = bufs
+    try:
         ctx.pileup(r, L, 0, k, nf, nf2, counts.ptr, cov.ptr, None, ent.ptr, sec.ptr)
         ctx.summary(cov.ptr, ent.ptr, L, work.ptr, out.ptr)
-        assert ctx.range_error() == -1, name
+        assert ctx.range_error() == -1
         hcov = cov.download(np.int32, L)
         hent = ent.download(np.float64, L)
         s = out.download(np.float64, 4)
         # checksum of checksums: all-M reads without N put every event into the coverage
-        assert int(hcov.sum(dtype=np.int64)) == synth.ref_events(rs, t), name
+        assert int(hcov.sum(dtype=np.int64)) == synth.ref_events(rs, t)
         c64 = hcov.astype(np.int64)
-        assert s[0] == np.mean(c64) and s[1] == np.mean(hent), name
-        assert int(s[2]) == int(np.count_nonzero(hcov)), name
+        assert s[0] == np.mean(c64) and s[1] == np.mean(hent)
+        assert int(s[2]) == int(np.count_nonzero(hcov))
         del c64
-        if name in full:
-            exp, (br, _) = O.bcount(L, 0, b)
-            assert br == -1
-            got = counts.download(np.int32, k * L).reshape(k, L)
-            assert np.array_equal(got, exp[:, :k].T), name
-            del got
-            ocov, opc, oent, osec = O.stats(exp, False, nthreads=T)
-            del opc, exp
-            assert np.array_equal(hcov, ocov), name
-            assert np.array_equal(hent, oent), name  # bit-identical (glibc log2 on the device)
-            assert np.array_equal(sec.download(np.float64, L), osec), name
-            del ocov, oent, osec
+        exp, (br, _) = O.bcount(L, 0, b)
+        assert br == -1
+        got = counts.download(np.int32, k * L).reshape(k, L)
+        assert np.array_equal(got, exp[:, :k].T)
+        del got
+        ocov, opc, oent, osec = O.stats(exp, False, nthreads=T)
+        del opc, exp
+        assert np.array_equal(hcov, ocov)
+        assert np.array_equal(hent, oent)  # bit-identical (glibc log2 on the device)
+        assert np.array_equal(sec.download(np.float64, L), osec)
+    finally:
         for x in bufs:
             x.free()
         r.free()
-        del hcov, hent
 
 
 @pytest.mark.parametrize("batch", [None, "200000"])

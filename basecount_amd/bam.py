@@ -173,6 +173,19 @@ class BamFile:
         return np.where(j & 1, byte & 0xF, byte >> 4)
 
 
+def find_ref_start(path: str, tid: int) -> int | None:
+    """Virtual offset of the first record whose refID is >= tid or -1 (None: the file ends
+    first), found without inflating the file (bcio_find_ref_start).  Exact for a file grouped by
+    reference; BamStream(voff_range=...) streams verify it (a wrong split fails their decode)."""
+    lib = N.bcio()
+    v = C.c_uint64()
+    rc = lib.bcio_find_ref_start(os.fsencode(path), int(tid), C.byref(v))
+    if rc == -1:
+        raise FileNotFoundError(lib.bcio_last_error().decode())
+    N.bcio_check(rc)
+    return int(v.value) or None
+
+
 class BamStream:
     """A BAM file decoded in batches of records (file order) with bounded memory: the
     reference's chunked read loop (main.py:142-162) without holding the file.
@@ -182,10 +195,18 @@ class BamStream:
                 ...
     """
 
-    def __init__(self, path: str, nthreads: int = 0):
+    def __init__(self, path: str, nthreads: int = 0, *, voff_range: tuple | None = None):
+        """``voff_range=(begin, end)``: only the records in [begin, end) (BAM virtual offsets,
+        ``find_ref_start``; end None: to the end of the file, begin None: no records)."""
         lib = N.bcio()
         h = C.c_void_p()
-        rc = lib.bcio_stream_open(os.fsencode(path), int(nthreads), C.byref(h))
+        if voff_range is None:
+            rc = lib.bcio_stream_open(os.fsencode(path), int(nthreads), C.byref(h))
+        else:
+            beg, end = voff_range
+            if beg is None:  # an empty range
+                beg, end = 1, 1
+            rc = lib.bcio_stream_open_range(os.fsencode(path), int(nthreads), int(beg), int(end or 0), C.byref(h))
         if rc == -1:
             raise FileNotFoundError(lib.bcio_last_error().decode())
         N.bcio_check(rc)

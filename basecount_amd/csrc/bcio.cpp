@@ -118,7 +118,9 @@ private:
 // Read-only mapping of the BAM file (read() into a buffer only if mmap is refused).
 class FileMap {
 public:
-    int open(const char* path, bool sequential = false) {
+    enum Advice { kWillNeed, kSequential, kRandom };
+    int open(const char* path, bool sequential = false) { return open_as(path, sequential ? kSequential : kWillNeed); }
+    int open_as(const char* path, Advice advice) {
         int fd = ::open(path, O_RDONLY | O_CLOEXEC);
         if (fd < 0) return -1;
         struct stat st;
@@ -130,7 +132,7 @@ public:
         if (n_) {
             void* m = mmap(nullptr, n_, PROT_READ, MAP_PRIVATE, fd, 0);
             if (m != MAP_FAILED) {
-                madvise(m, n_, sequential ? MADV_SEQUENTIAL : MADV_WILLNEED);
+                madvise(m, n_, advice == kSequential ? MADV_SEQUENTIAL : advice == kRandom ? MADV_RANDOM : MADV_WILLNEED);
                 map_ = (const uint8_t*)m;
             } else {
                 buf_.resize(n_);
@@ -795,7 +797,10 @@ struct bcio_stream {
     uint64_t dropped = 0;  // mapping bytes already given back
     double rec_bytes = 0.0;  // mean inflated bytes per record so far
     int64_t returned = 0;
-    bool all_read() const { return coff >= file.size(); }
+    // range streams (bcio_stream_open_range): blocks are scanned below cend only, and the block at
+    // tail_block (if any) keeps its first tail_keep inflated bytes
+    uint64_t cend = UINT64_MAX, tail_block = UINT64_MAX, tail_keep = 0;
+    bool all_read() const { return coff >= std::min<uint64_t>(cend, file.size()); }
     const uint8_t* base() const { return pend ? pend->data() + pbeg : nullptr; }
     uint64_t avail() const { return pend_n - pbeg; }
 };
@@ -807,8 +812,9 @@ int stream_fill(bcio_stream* s, uint64_t want) {
     const uint8_t* comp = s->file.data();
     const uint64_t n = s->file.size();
     std::vector<Block> blocks;
-    uint64_t off = s->coff, uoff = 0;
-    while (off < n && uoff < want) {
+    uint64_t off = s->coff, uoff = 0, trim = 0;
+    const uint64_t lim = std::min<uint64_t>(n, s->cend);
+    while (off < lim && uoff < want) {
         Block b;
         uint64_t bsize = 0;
         int rc = scan_block(comp + off, n - off, &b, &bsize);
@@ -818,6 +824,10 @@ int stream_fill(bcio_stream* s, uint64_t want) {
         b.uoff = uoff;
         uoff += b.isize;
         blocks.push_back(b);
+        if (off == s->tail_block) {  // the range ends inside this block
+            if (s->tail_keep > b.isize) return fail(BCIO_E_ARG, "range end past its block");
+            trim = b.isize - s->tail_keep;
+        }
         off += bsize;
     }
     // one buffer: the bytes not handed out yet, then the new blocks' bytes
@@ -827,7 +837,7 @@ int stream_fill(bcio_stream* s, uint64_t want) {
     if (keep) std::memcpy(next->data(), s->base(), keep);
     if (!inflate_blocks(comp, blocks, next->data() + keep, s->nthreads)) return fail(BCIO_E_ZLIB, "inflate failed");
     s->pend = std::move(next);
-    s->pend_n = keep + uoff;
+    s->pend_n = keep + uoff - trim;
     s->pbeg = 0;
     s->coff = off;
     // give the consumed compressed pages back (whole pages below the next block)
@@ -853,7 +863,7 @@ extern "C" int bcio_stream_open(const char* path, int nthreads, bcio_stream** ou
     if (orc == -1) return fail(BCIO_E_IO, std::string("cannot open ") + path);
     if (orc != 0) return fail(BCIO_E_IO, "short read");
     s->nthreads = hw_threads(nthreads);
-    uint64_t want = 4u << 20;
+    uint64_t want = 256u << 10;
     for (;;) {  // the header, however many blocks it takes
         uint64_t q = 0;
         int rc = parse_header(s->base(), s->avail(), s->names, s->lens, &q);
@@ -925,6 +935,255 @@ extern "C" void bcio_stream_close(bcio_stream* s) {
     } catch (...) {
         delete s;
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Record-aligned split points for decoding one file on several ranks (bcio.h: sharded decode).
+// Virtual offsets as in a BAM index: (block file offset << 16) | offset in its inflated bytes.
+namespace {
+
+// Inflated bytes of consecutive blocks, with where each block lies in the file and in buf.
+struct Span {
+    std::vector<uint8_t> buf;
+    std::vector<uint64_t> boff, ustart;
+    uint64_t next = 0;  // file offset after the last block
+    bool eof = false;
+};
+
+// append blocks from sp.next until buf holds >= want bytes (or the file ends); single thread
+int span_grow(const uint8_t* comp, uint64_t n, Span& sp, uint64_t want) {
+    while (!sp.eof && sp.buf.size() < want) {
+        if (sp.next >= n) {
+            sp.eof = true;
+            break;
+        }
+        Block b;
+        uint64_t bsize = 0;
+        int rc = scan_block(comp + sp.next, n - sp.next, &b, &bsize);
+        if (rc == 1) return fail(BCIO_E_FORMAT, g_err);
+        if (rc != BCIO_OK) return rc;
+        b.coff += sp.next;
+        b.uoff = sp.buf.size();
+        sp.boff.push_back(sp.next);
+        sp.ustart.push_back(b.uoff);
+        sp.buf.resize(b.uoff + b.isize);
+        if (!inflate_blocks(comp, std::vector<Block>{b}, sp.buf.data(), 1)) return fail(BCIO_E_ZLIB, "inflate failed");
+        sp.next += bsize;
+    }
+    return BCIO_OK;
+}
+
+// virtual offset of byte u of the span (a record start); u at the very end: the next block
+uint64_t span_voff(const Span& sp, uint64_t u) {
+    if (u >= sp.buf.size()) return sp.next << 16;
+    size_t j = (size_t)(std::upper_bound(sp.ustart.begin(), sp.ustart.end(), u) - sp.ustart.begin()) - 1;
+    // an empty block shares its start with the next one: take the last block starting at or before u
+    return (sp.boff[j] << 16) | (u - sp.ustart[j]);
+}
+
+// the record at p[q, N) looks like a BAM record of a file with n_ref references: its size
+// (4 + block_size), 0 if not (or if it is cut off by N)
+uint64_t plausible_record(const uint8_t* p, uint64_t q, uint64_t N, int32_t n_ref) {
+    if (q + 36 > N) return 0;
+    const uint32_t bs = rd32(p + q);
+    if (bs < 32 || bs > (1u << 28) || q + 4 + bs > N) return 0;
+    const uint8_t* r = p + q + 4;
+    const int32_t tid = rd32s(r), pos = rd32s(r + 4), ls = rd32s(r + 16), ntid = rd32s(r + 20), npos = rd32s(r + 24);
+    const uint8_t lrn = r[8];
+    if (tid < -1 || tid >= n_ref || ntid < -1 || ntid >= n_ref || pos < -1 || npos < -1 || ls < 0 || lrn < 1) return 0;
+    if (32ull + lrn + 4ull * rd16(r + 12) + (((uint64_t)ls + 1) / 2) + (uint64_t)ls > bs) return 0;
+    const uint8_t* nm = r + 32;
+    if (nm[lrn - 1] != 0) return 0;
+    for (int i = 0; i + 1 < lrn; ++i)
+        if (nm[i] < 33 || nm[i] > 126) return 0;
+    return 4ull + bs;
+}
+
+// the first offset in [0, lim) where a chain of 4 plausible records starts (or one that ends
+// exactly at the end of the file's data), -1 if none
+int64_t sync_records(const Span& sp, uint64_t lim, int32_t n_ref) {
+    const uint8_t* p = sp.buf.data();
+    const uint64_t N = sp.buf.size();
+    for (uint64_t o = 0; o < lim && o < N; ++o) {
+        uint64_t q = o;
+        int k = 0;
+        while (k < 4) {
+            const uint64_t sz = plausible_record(p, q, N, n_ref);
+            if (!sz) break;
+            q += sz;
+            ++k;
+            if (q == N && sp.eof) break;
+        }
+        if (k >= 4 || (k >= 1 && q == N && sp.eof)) return (int64_t)o;
+    }
+    return -1;
+}
+
+// the first BGZF block header at or after x whose chain of three blocks parses (or reaches the
+// end of the file), -1 if none
+int64_t sync_block(const uint8_t* comp, uint64_t n, uint64_t x) {
+    for (uint64_t o = x; o + 18 <= n; ++o) {
+        if (comp[o] != 31 || comp[o + 1] != 139 || comp[o + 2] != 8 || !(comp[o + 3] & 4)) continue;
+        uint64_t q = o;
+        int k = 0;
+        bool ok = true;
+        while (k < 3 && q < n) {
+            Block b;
+            uint64_t bsize = 0;
+            if (scan_block(comp + q, n - q, &b, &bsize) != BCIO_OK) {
+                ok = false;
+                break;
+            }
+            q += bsize;
+            ++k;
+        }
+        if (ok && (k == 3 || q == n)) return (int64_t)o;
+    }
+    return -1;
+}
+
+// the header of a mapped file: reference count and the first record's virtual offset
+int header_span(const uint8_t* comp, uint64_t n, int32_t* n_ref, uint64_t* first) {
+    Span sp;
+    std::vector<std::string> names;
+    std::vector<int64_t> lens;
+    for (uint64_t want = 65536;; want *= 2) {
+        int rc = span_grow(comp, n, sp, want);
+        if (rc != BCIO_OK) return rc;
+        uint64_t q = 0;
+        rc = parse_header(sp.buf.data(), sp.buf.size(), names, lens, &q);
+        if (rc == BCIO_OK) {
+            *n_ref = (int32_t)names.size();
+            *first = span_voff(sp, q);
+            return BCIO_OK;
+        }
+        if (rc < 0) return rc;
+        if (sp.eof) return fail(BCIO_E_FORMAT, g_err);
+    }
+}
+
+}  // namespace
+
+extern "C" int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff) {
+    if (!path || !voff) return fail(BCIO_E_ARG, "null argument");
+    FileMap fm;
+    const int orc = fm.open_as(path, FileMap::kRandom);  // a few probes: no readahead of the file
+    if (orc == -1) return fail(BCIO_E_IO, std::string("cannot open ") + path);
+    if (orc != 0) return fail(BCIO_E_IO, "short read");
+    const uint8_t* comp = fm.data();
+    const uint64_t n = fm.size();
+    int32_t n_ref = 0;
+    uint64_t first = 0;
+    int rc = header_span(comp, n, &n_ref, &first);
+    if (rc != BCIO_OK) return rc;
+    // lo: a record start (virtual offset) whose refID is below tid; the boundary lies after it
+    uint64_t lo = first;
+    // hi: a file offset such that the first record synchronised in any block at or after it has
+    // refID >= tid (or -1); the bisection narrows [lo's block, hi) to a few blocks
+    uint64_t hi = n;
+    auto ref_at = [&](uint64_t v, int32_t* ref, bool* end) -> int {  // refID of the record at v
+        Span sp;
+        sp.next = v >> 16;
+        const uint64_t u = v & 0xFFFF;
+        int rc2 = span_grow(comp, n, sp, u + 36);
+        if (rc2 != BCIO_OK) return rc2;
+        *end = sp.buf.size() <= u;
+        *ref = *end ? -1 : (sp.buf.size() >= u + 8 ? rd32s(sp.buf.data() + u + 4) : -2);
+        return *ref == -2 ? fail(BCIO_E_FORMAT, "truncated BAM record") : BCIO_OK;
+    };
+    {
+        int32_t r0 = 0;
+        bool end = false;
+        if ((rc = ref_at(first, &r0, &end)) != BCIO_OK) return rc;
+        if (tid <= 0 || end || r0 < 0 || r0 >= tid) {
+            *voff = end ? 0 : first;
+            return BCIO_OK;
+        }
+    }
+    constexpr uint64_t kProbe = 4u << 20;
+    while (hi > (lo >> 16) + 4 * 65536) {
+        const uint64_t mid = (lo >> 16) + (hi - (lo >> 16)) / 2;
+        const int64_t c = sync_block(comp, n, mid);
+        if (c < 0 || (uint64_t)c >= hi) {
+            hi = mid;
+            continue;
+        }
+        Span sp;
+        sp.next = (uint64_t)c;
+        int64_t o = -1;
+        for (uint64_t want = 1; o < 0 && want <= kProbe; want *= 4) {  // one block, more if a record is longer
+            if ((rc = span_grow(comp, n, sp, want)) != BCIO_OK) return rc;
+            o = sync_records(sp, sp.buf.size(), n_ref);
+            if (sp.eof) break;
+        }
+        if (o < 0) {  // no record start found (a record longer than the probe): look lower
+            hi = mid;
+            continue;
+        }
+        const int32_t ref = rd32s(sp.buf.data() + o + 4);
+        if (ref >= 0 && ref < tid) lo = std::max(lo, span_voff(sp, (uint64_t)o));
+        else hi = (uint64_t)c;
+    }
+    // hop records from lo to the first with refID >= tid or -1 (or the end of the file)
+    Span sp;
+    sp.next = lo >> 16;
+    uint64_t u = lo & 0xFFFF;
+    for (;;) {
+        if ((rc = span_grow(comp, n, sp, u + 36)) != BCIO_OK) return rc;
+        if (u >= sp.buf.size()) {
+            *voff = 0;  // no such record: the range runs to the end of the file
+            return BCIO_OK;
+        }
+        if (u + 8 > sp.buf.size()) return fail(BCIO_E_FORMAT, "truncated BAM record");
+        const int32_t ref = rd32s(sp.buf.data() + u + 4);
+        if (ref < 0 || ref >= tid) {
+            *voff = span_voff(sp, u);
+            return BCIO_OK;
+        }
+        const uint32_t bs = rd32(sp.buf.data() + u);
+        if (bs < 32) return fail(BCIO_E_FORMAT, "truncated BAM record");
+        u += 4ull + bs;
+        // keep the span bounded: drop whole blocks before u
+        if (u > (4u << 20) && sp.ustart.size() > 1) {
+            size_t j = (size_t)(std::upper_bound(sp.ustart.begin(), sp.ustart.end(), u) - sp.ustart.begin()) - 1;
+            const uint64_t cut = sp.ustart[j];
+            sp.buf.erase(sp.buf.begin(), sp.buf.begin() + (int64_t)cut);
+            sp.boff.erase(sp.boff.begin(), sp.boff.begin() + (int64_t)j);
+            sp.ustart.erase(sp.ustart.begin(), sp.ustart.begin() + (int64_t)j);
+            for (auto& x : sp.ustart) x -= cut;
+            u -= cut;
+        }
+    }
+}
+
+extern "C" int bcio_stream_open_range(const char* path, int nthreads, uint64_t voff_begin, uint64_t voff_end,
+                                      bcio_stream** out) {
+    int rc = bcio_stream_open(path, nthreads, out);
+    if (rc != BCIO_OK) return rc;
+    bcio_stream* s = *out;
+    // the records of [voff_begin, voff_end): restart the block scan at voff_begin's block
+    s->pend.reset();
+    s->pend_n = s->pbeg = 0;
+    hop_reset(s->hop);
+    s->coff = voff_begin >> 16;
+    if (voff_end) {
+        s->tail_block = voff_end >> 16;
+        s->tail_keep = voff_end & 0xFFFF;
+        s->cend = s->tail_keep ? s->tail_block + 1 : s->tail_block;
+        if (!s->tail_keep) s->tail_block = UINT64_MAX;
+    }
+    const uint64_t skip = voff_begin & 0xFFFF;
+    if (voff_end && voff_end <= voff_begin) {  // an empty range
+        s->coff = s->cend;
+        return BCIO_OK;
+    }
+    if ((rc = stream_fill(s, skip + 1)) != BCIO_OK || s->avail() < skip) {
+        bcio_stream_close(s);
+        *out = nullptr;
+        return rc != BCIO_OK ? rc : fail(BCIO_E_ARG, "range start past its block");
+    }
+    s->pbeg = skip;
+    return BCIO_OK;
 }
 
 // ------------------------------------------------------------------------------------------

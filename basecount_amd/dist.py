@@ -299,6 +299,50 @@ def shard(refs: list[str], weights: dict, world: int) -> dict:
     return owner
 
 
+def shard_contiguous(weights: list, world: int) -> list[int]:
+    """Cuts b[0] = 0 <= b[1] <= ... <= b[world] = n of items 0..n-1 (references in file order)
+    into `world` contiguous runs, rank r owning [b[r], b[r + 1]): the smallest largest-run weight
+    (binary search on it, runs filled greedily), then the runs spread so that no rank is left
+    empty while another holds two or more items."""
+    n = len(weights)
+    w = [max(0, int(x)) + 1 for x in weights]  # +1: unrequested / empty references still cost a little
+
+    def runs(cap):
+        cuts, load = [0], 0
+        for i, x in enumerate(w):
+            if load + x > cap and load > 0:
+                cuts.append(i)
+                load = 0
+            load += x
+        return cuts
+
+    lo, hi = max(w, default=1), max(1, sum(w))
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if len(runs(mid)) <= world:
+            hi = mid
+        else:
+            lo = mid + 1
+    cuts = runs(lo)
+    # more ranks than runs: split the runs with several items (largest first) while they last
+    while len(cuts) < world:
+        bounds = cuts + [n]
+        best = max(range(len(cuts)), key=lambda i: (bounds[i + 1] - bounds[i] > 1,
+                                                      sum(w[bounds[i]:bounds[i + 1]]), -i))
+        a, b = bounds[best], bounds[best + 1]
+        if b - a < 2:
+            break
+        half, acc, m = sum(w[a:b]) / 2, 0, a + 1
+        for i in range(a, b - 1):
+            acc += w[i]
+            m = i + 1
+            if acc >= half:
+                break
+        cuts.insert(best + 1, m)
+    cuts += [n] * (world + 1 - len(cuts))
+    return cuts
+
+
 def _stdout_bytes(data: bytes) -> None:
     sys.stdout.flush()
     sys.stdout.buffer.write(data)

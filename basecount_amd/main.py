@@ -26,13 +26,14 @@ import json
 import ctypes as C
 import math
 import os
+import sys
 from array import array
 
 import numpy as np
 
 from . import device as D
 from . import fmt
-from .bam import REC_BAD_CLIP, REC_NEG_POS, REC_NO_CIGAR, REC_NO_QUAL, REC_NO_SEQ, BamFile, BamStream
+from .bam import REC_BAD_CLIP, REC_NEG_POS, REC_NO_CIGAR, REC_NO_QUAL, REC_NO_SEQ, BamFile, BamStream, find_ref_start
 from .scheme import load_scheme
 from .version import __version__
 
@@ -490,6 +491,17 @@ class _Ungrouped(Exception):
     by reference): start again, accumulating every reference until the end of the file."""
 
 
+class _ShardMiss(Exception):
+    """Sharded decode: this rank's byte range of the file did not hold exactly its references'
+    records (file not grouped by reference, or a split the record chain does not confirm)."""
+
+
+def _shard_decode_on(group) -> bool:
+    """BASECOUNT_SHARD_DECODE: 0 every rank decodes the whole file; 1 (default) each rank its
+    byte range, falling back to the whole file if a range misses; require: a miss is an error."""
+    return group is not None and group.world > 1 and os.environ.get("BASECOUNT_SHARD_DECODE", "1") != "0"
+
+
 def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality=0,
                    chunk_size=1000000, show_n_bases=False, long_format=False, *, device=None,
                    _mode="rows", _tiles=None, _group=None):
@@ -508,6 +520,17 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
     returns ``(results, owner, order)``; every rank raises the same first error."""
     args = (bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
             long_format, device, _mode, _tiles, _group)
+    if _shard_decode_on(_group):
+        # each rank inflates and decodes only the byte range of its own references (a file
+        # grouped by reference); None: some rank's range did not confirm, all decode everything
+        res = _get_basecounts(*args, grouped=True, sharded=True)
+        if res is not None:
+            return res
+        if os.environ.get("BASECOUNT_SHARD_DECODE") == "require":  # tests: the split must hold
+            raise RuntimeError("sharded decode: a rank's byte range did not hold exactly its references")
+        if os.environ.get("BASECOUNT_HIP_TIMING"):
+            print(f"basecount[{_group.rank}] sharded decode missed: every rank decodes the file",
+                  file=sys.stderr)
     try:
         return _get_basecounts(*args, grouped=True)
     except _Ungrouped:
@@ -515,7 +538,7 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
 
 
 def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
-                    long_format, device, _mode, _tiles, _group, grouped):
+                    long_format, device, _mode, _tiles, _group, grouped, sharded=False):
     stream = BamStream(bam)
     try:
         references = get_references(stream, references)
@@ -536,7 +559,30 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         ncols = k  # N is only ever reported with show_n_bases
         owner = None
         mine = ref_order
-        if _group is not None:
+        t_lo, t_hi = 0, len(names)  # the refIDs this rank's byte range holds (sharded decode)
+        if sharded:
+            from .dist import shard_contiguous
+
+            # contiguous refID runs per rank (file order), balanced on the requested references'
+            # lengths; each rank streams only the bytes from its first reference's first record
+            # to the next rank's (the last rank: to the end of the file, unmapped reads included)
+            cuts = shard_contiguous([int(stream.lengths[t]) if wanted_t else 0
+                                     for t, wanted_t in enumerate(n in references for n in names)], _group.world)
+            owner = {r: next(i for i in range(_group.world) if cuts[i] <= ref_index[r] < cuts[i + 1])
+                     for r in ref_order}
+            mine = [r for r in ref_order if owner[r] == _group.rank]
+            t_lo, t_hi = cuts[_group.rank], cuts[_group.rank + 1]
+            last = _group.rank == _group.world - 1
+            with _phase("decode"):
+                beg = find_ref_start(bam, t_lo)
+                end = None if last else find_ref_start(bam, t_hi)
+                if beg is None or (end is not None and end <= beg):
+                    beg = end = None  # no records in this rank's range
+                stream.close()
+                stream = BamStream(bam, voff_range=(beg, end))
+            if last:
+                t_hi = len(names)
+        elif _group is not None:
             from .dist import shard
 
             # cost estimate before any read is seen: the per-position outputs (linear in length)
@@ -556,14 +602,28 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         def tiles_of(ref):
             return _tiles(ref) if _tiles else None
 
-        base = 0  # accepted reads before the current batch (global ordinals)
+        base = 0  # accepted reads before the current batch (global ordinals; sharded: in the range)
         cur = nxt = None
+        miss = False
+
+        def next_batch():
+            if not sharded:
+                return stream.next_batch(B)
+            try:
+                return stream.next_batch(B)
+            except (ValueError, OSError) as e:  # the record chain did not fit the range
+                raise _ShardMiss() from e
+
         try:
             with _phase("decode"):
-                cur = stream.next_batch(B)
+                cur = next_batch()
             sel_next = None
             while cur is not None:
                 f = cur
+                if sharded and f.n_records:
+                    tids = f.tid
+                    if bool(np.any(((tids < t_lo) | (tids >= t_hi)) & (tids != -1))):
+                        raise _ShardMiss()
                 with _phase("select"):
                     sel = sel_next if sel_next is not None else f.select(mmq, wanted)
                 sel_next = None
@@ -591,10 +651,10 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 # one batch of look-ahead: a reference absent from the next batch is complete
                 # (in a file grouped by reference); none after the reference's first in-loop fault
                 with _phase("decode"):
-                    nxt = stream.next_batch(B) if fl.inloop() is None else None
+                    nxt = next_batch() if fl.inloop() is None else None
                 if ctx is not None and here:
                     if any(r in finished for r in here):
-                        raise _Ungrouped()
+                        raise _ShardMiss() if sharded else _Ungrouped()
                     with _phase("select"):
                         nsel = sel_next = nxt.select(mmq, wanted) if (nxt is not None and grouped) else None
                     with _phase("upload"):
@@ -642,6 +702,8 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                     else:  # no reads at all
                         results[ref], _ = _device_reference(ctx, _no_reads(), L, mbq, ncols, k, nf, nf2,
                                                             _mode, tiles_of(ref), _tiles is not None, scratch)
+        except _ShardMiss:
+            miss = True
         finally:
             for b in (cur, nxt):
                 if b is not None:
@@ -650,7 +712,10 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 ctx.sync()
             for b in acc.values():
                 b.free()
-        if _group is not None and mbq_ok:
+        if sharded:
+            if not _merge_shards(_group, fl, miss, base, ref_order, owner, names, nreads):
+                return None  # some rank's range did not confirm: every rank decodes the file
+        elif _group is not None and mbq_ok:
             # every rank needs every reference's first out-of-range read to raise the same error
             flat = [v for r in ref_order for v in fl.range_.get(r, (-2, -1))]
             alls = _group.all_gather_ints(flat)
@@ -676,6 +741,50 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         return out
     finally:
         stream.close()
+
+
+def _merge_shards(group, fl: _Faults, miss: bool, n_accepted: int, ref_order, owner, names, nreads) -> bool:
+    """Sharded decode: turn this rank's range-local fault ordinals into the file's (each range
+    starts after the accepted reads of the ranges before it) and give every rank the faults the
+    whole file holds, as one process streaming it would have recorded them.  False (on every rank)
+    if any rank's range missed."""
+    stopped = fl.inloop() is not None  # this range stopped at its first in-loop fault
+    vals = [0 if miss else 1, int(stopped), fl.n_records, n_accepted,
+            fl.keyerror[0] if fl.keyerror else -1,
+            names.index(fl.keyerror[1]) if fl.keyerror and fl.keyerror[1] in names else -1,
+            fl.clip if fl.clip is not None else -1]
+    for r in ref_order:
+        rg = fl.range_.get(r, (-1, -1))
+        vals += [fl.type_ord.get(r, -1), rg[0], rg[1], nreads[r]]
+    alls = group.all_gather_ints(vals)
+    if any(v[0] == 0 for v in alls):
+        return False
+    # a range that stopped at an in-loop fault counted only part of its reads: the ranges after
+    # it hold only later faults, which cannot change what is raised first
+    cut = next((i for i, v in enumerate(alls) if v[1]), len(alls) - 1)
+    bases = [0]
+    for v in alls[:-1]:
+        bases.append(bases[-1] + v[3])
+    fl.n_records = sum(v[2] for v in alls)
+    fl.keyerror = fl.clip = None
+    fl.type_ord, fl.range_ = {}, {}
+    for i in range(cut + 1):
+        v, b = alls[i], bases[i]
+        if v[4] >= 0 and fl.keyerror is None:
+            fl.keyerror = (b + v[4], names[v[5]] if v[5] >= 0 else None)
+        if v[6] >= 0 and fl.clip is None:
+            fl.clip = b + v[6]
+    for j, r in enumerate(ref_order):
+        i = owner[r]
+        v = alls[i]
+        nreads[r] = v[7 + 4 * j + 3]
+        if i > cut:
+            continue
+        if v[7 + 4 * j] >= 0:
+            fl.type_ord[r] = bases[i] + v[7 + 4 * j]
+        if v[7 + 4 * j + 1] >= 0:
+            fl.range_[r] = (bases[i] + v[7 + 4 * j + 1], v[7 + 4 * j + 2])
+    return True
 
 
 def _no_reads() -> D.BcReads:

@@ -120,6 +120,22 @@ const char* bcio_stream_ref_name(const bcio_stream* s, int32_t i);
 int64_t bcio_stream_ref_len(const bcio_stream* s, int32_t i);
 void bcio_stream_close(bcio_stream* s);
 
+/* ---- one file decoded by several ranks (each only its own references' records) ----------------
+ * Positions are BAM virtual offsets: (BGZF block file offset << 16) | offset in its inflated bytes.
+ * bcio_find_ref_start: the position of the first record whose refID is >= tid or -1 (unmapped),
+ * 0 if there is none (the file ends first).  The file is not inflated: a bisection over the BGZF
+ * blocks (each probe finds a block header and then a record start by validating a chain of
+ * records) narrows the search to a few blocks, which are then hopped record by record.  The
+ * answer is exact when the file is grouped by reference (coordinate-sorted) and the probes
+ * synchronised correctly; neither is assumed: a caller verifies them with the range streams.
+ * bcio_stream_open_range: a stream over the records of [voff_begin, voff_end) (voff_end 0: to the
+ * end of the file; voff_end <= voff_begin otherwise: no records) with the header's references.
+ * voff_begin must be a record start.  If the record chain does not end exactly at voff_end,
+ * bcio_stream_next fails with BCIO_E_FORMAT ("truncated BAM record"): the split was wrong. */
+int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff);
+int bcio_stream_open_range(const char* path, int nthreads, uint64_t voff_begin, uint64_t voff_end,
+                           bcio_stream** out);
+
 /* BAM-packed SEQ bytes -> BC_SEQ_EVENT (basecount_hip.h), on the host with `nthreads` threads
  * (<= 0: hardware).  out_bytes >= nbytes rounded up to 16 plus 16; the tail is zero-filled.
  * The decoder already provides this layout for a file's records (bcio_records.seq_event).   */

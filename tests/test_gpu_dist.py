@@ -8,6 +8,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -124,3 +125,102 @@ def test_bench_gpus_2_rehearsal():
     assert d["n_gpus"] == 2 and d["config"]["comm"] == "gloo" and d["parity_vs_oracle"]
     c5 = d["extra"]["c5"]
     assert c5["parity_vs_oracle"] and c5["gather_bytes"] == 32 * 24 and c5["scaling"] == "strong"
+
+
+# ------------------------------------------------------------------ sharded decode
+CONTIGS6 = [("c0", 30_000), ("c1", 5_000), ("c2", 80_000), ("c3", 12_000), ("c4", 50_000), ("c5", 9_000)]
+
+
+def _ranks(world, args, tmp_path, name, extra_env=None, cwd=None):
+    """Run the CLI on `world` ranks (gloo); (return codes, stdout bytes, stderr texts)."""
+    out = tmp_path / f"{name}.out"
+    env = dict(os.environ, PYTHONPATH=REPO, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
+               BASECOUNT_DIST_BACKEND="gloo", PYTHONHASHSEED="0", **(extra_env or {}))
+    with open(out, "wb") as fh:
+        procs = []
+        for r in range(world):
+            e = dict(env, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r)) if world > 1 else env
+            procs.append(subprocess.Popen([sys.executable, "-m", "basecount_amd", *args], stdout=fh,
+                                          stderr=subprocess.PIPE, env=e, cwd=cwd))
+        errs = [p.communicate(timeout=600)[1].decode() for p in procs]
+    return [p.returncode for p in procs], out.read_bytes(), errs
+
+
+def _last_line(err: str) -> str:
+    """The exception line (torch.distributed prefixes a rank's traceback lines with [rankN]:)."""
+    import re
+
+    lines = [re.sub(r"^\[rank\d+\]:\s*", "", ln) for ln in err.strip().splitlines() if ln.strip()]
+    return lines[-1] if lines else ""
+
+
+@pytest.fixture(scope="module")
+def shard_bams(tmp_path_factory):
+    from basecount_amd import synth
+
+    d = tmp_path_factory.mktemp("shard")
+    rs = synth.make_reads(CONTIGS6, 4_000, True, 21)
+    ok = str(d / "grouped.bam")
+    synth.write_bam(rs, ok)
+    # one read of c3 (its last: the file stays sorted) runs past the reference end
+    last_c3 = int(np.flatnonzero(rs.tid == 3)[-1])
+    rs.pos[last_c3] = CONTIGS6[3][1] - 10
+    bad = str(d / "range_error.bam")
+    synth.write_bam(rs, bad)
+    return ok, bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_decode_cli_matches_one_process(shard_bams, tmp_path, world):
+    """Each rank decodes only its references' byte range (BASECOUNT_SHARD_DECODE=require: a
+    range that misses is an error); output and errors byte-identical to one process, also in
+    2,500-record batches (the ranges stream) and with a KeyError / IndexError to raise."""
+    ok, bad = shard_bams
+    cases = [(ok, []), (ok, ["--summarise"]), (ok, ["--min-base-quality", "20", "--show-n-bases", "--long-format"]),
+             (ok, ["--references", "c2", "c4"]), (ok, ["--chunk-size", "3000", "--min-mapping-quality", "30"]),
+             (bad, []), (bad, ["--summarise"])]
+    for i, (bam, args) in enumerate(cases):
+        rc1, out1, err1 = _ranks(1, [bam, *args], tmp_path, f"s{i}")
+        for batch in (None, "2500"):
+            env = {"BASECOUNT_SHARD_DECODE": "require"}
+            if batch:
+                env["BASECOUNT_BATCH_RECORDS"] = batch
+            rcn, outn, errn = _ranks(world, [bam, *args], tmp_path, f"m{i}{batch}", env)
+            if rc1[0] == 0:
+                assert rcn == [0] * world, (args, [e[-1500:] for e in errn])
+                assert outn == out1, args
+            else:
+                assert all(r != 0 for r in rcn), (args, rcn)
+                assert _last_line(errn[0]) == _last_line(err1[0]), (args, errn[0][-800:])
+                assert outn == out1 == b""
+
+
+@pytest.mark.gpu
+def test_sharded_decode_halves_the_c5_decode(tmp_path):
+    """C5 (24 contigs, 1.2 M reads) --summarise on two ranks, each decoding
+    its half of the file: the slower rank's decode phase well under one process's, output
+    identical."""
+    import re
+
+    from basecount_amd import synth
+
+    bam = str(tmp_path / "c5.bam")
+    synth.write_bam(synth.make_config("c5"), bam)
+    env = {"BASECOUNT_HIP_TIMING": "1", "BASECOUNT_SHARD_DECODE": "require"}
+
+    def decode_ms(err):
+        m = re.findall(r"host decode: ([0-9.]+) ms", err)
+        assert m, err[-1500:]
+        return float(m[-1])
+
+    best1, best2 = [], []
+    for rep in range(2):  # the first run of each pays the page cache / library warm-up
+        rc1, out1, err1 = _ranks(1, [bam, "--summarise"], tmp_path, f"one{rep}", env)
+        rc2, out2, err2 = _ranks(2, [bam, "--summarise"], tmp_path, f"two{rep}", env)
+        assert rc1 == [0] and rc2 == [0, 0], (err1[0][-1500:], [e[-1500:] for e in err2])
+        assert out2 == out1
+        best1.append(decode_ms(err1[0]))
+        best2.append(max(decode_ms(e) for e in err2))
+    print(f"C5 decode: one rank {min(best1):.1f} ms, two ranks (slower) {min(best2):.1f} ms")
+    assert min(best2) < 0.75 * min(best1), (best1, best2)

@@ -206,6 +206,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     int64_t bad = INT64_MAX;
 
+    // run records (bc_reads.read_runs) in place of the first decode: the variants with spare
+    // registers (the others spill with the extra path)
+    constexpr bool kRunsOn = !QUAL && NC == 5;
     // the next chunk's per-read fields are loaded while the current one is walked
     uint32_t fpos = 0x7FFFFFFFu, fsn = 0, fcb = 0, fcn = 0, fsn_first = 0, fsn_last = 0;
     auto fetch_fields = [&](int64_t ch) {
@@ -214,8 +217,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const int n = (int)(A.n - b0 < kRcReads ? A.n - b0 : kRcReads);
         if (tid < n) {
             fpos = (uint32_t)A.pos[b0 + tid];
-            fcb = A.cig_beg[b0 + tid];
-            fcn = A.cig_n[b0 + tid];
+            if (!kRunsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
+                fcb = A.cig_beg[b0 + tid];
+                fcn = A.cig_n[b0 + tid];
+            }
             fsn = A.seq_nib[b0 + tid];
         }
         fsn_first = A.seq_nib[b0];  // speculative staging bounds (reads usually lie in file order)
@@ -225,9 +230,6 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
     // with qualities and six columns, which sit at the VGPR cap without it
     constexpr bool kPfOn = !(QUAL && NC == 6);
-    // run records (bc_reads.read_runs) in place of the first decode: the variants with spare
-    // registers (the others spill with the extra path)
-    constexpr bool kRunsOn = !QUAL && NC == 5;
     const uint4* const runs = kRunsOn ? A.runs : nullptr;
     // the upload's chunk summaries: the chunk bounds without the block reduction (and its barrier)
     const uint4* const sums = kRunsOn && A.runs ? A.sums : nullptr;
@@ -286,9 +288,16 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         T.span = T.qlen = 0;
 #pragma unroll
         for (int i = 0; i < kMaxRuns; ++i) T.st[i] = T.en[i] = 0, T.qd[i] = 0;
-        const int cmax = (int)U(wave_reduce<true>(valid ? (mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre) : 0u));
+        // the CIGAR fields of a chunk read from run records: loaded only when a decode needs them
+        auto cig_fields = [&]() {
+            if (runs && valid) {
+                mcb = A.cig_beg[c0 + tid];
+                mcn = A.cig_n[c0 + tid];
+            }
+        };
         // the first two runs only (all the event image needs); a chunk with more re-decodes below
         auto decode = [&](auto nslot) {
+            const int cmax = (int)U(wave_reduce<true>(valid ? (mcn < (uint32_t)kPre ? mcn : (uint32_t)kPre) : 0u));
             if (valid) {
                 uint32_t w[kPre];
                 const bool use_pf = kPfOn && pf_ok && !runs && cmax <= kPf;  // (uniform)
@@ -330,6 +339,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // and maxima over the simple reads
         uint32_t cspan = T.span;
         if (cx && !sums) {
+            cig_fields();
             uint64_t sp = 0;
             for (uint32_t k = 0; k < mcn; ++k) {
                 const uint32_t wk = A.cigar[mcb + k];
@@ -364,7 +374,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const uint32_t seg_hi = v[3];
         const int maxspan = (int)v[4], maxrun = (int)v[5];
         const bool gap = v[6] != 0;
-        if (maxrun > 2) decode(std::integral_constant<int, kMaxRuns>{});  // (uniform) full run tables
+        if (maxrun > 2) {  // (uniform) full run tables
+            cig_fields();
+            decode(std::integral_constant<int, kMaxRuns>{});
+        }
         seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
         if (cx) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
@@ -423,7 +436,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 rec[tid * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
                 rec[tid * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
             }
-            rpos[tid] = (int32_t)mpos;
+            if (!img_path) rpos[tid] = (int32_t)mpos;  // (the window tables of the run-table walk)
         }
         if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
         __syncthreads();  // stage, records and the complex-read list complete

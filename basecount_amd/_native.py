@@ -128,6 +128,7 @@ def bcio() -> C.CDLL:
     lib.bcio_stream_close.argtypes = [C.c_void_p]
     lib.bcio_stream_close.restype = None
     lib.bcio_find_ref_start.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.c_uint64)]
+    lib.bcio_find_record.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint64)]
     lib.bcio_stream_open_range.argtypes = [C.c_char_p, C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p)]
     lib.bcio_write_bam.argtypes = [C.c_char_p, C.POINTER(BcioWriteSpec)]
     lib.bcio_seq_to_event.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int]

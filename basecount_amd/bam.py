@@ -173,13 +173,17 @@ class BamFile:
         return np.where(j & 1, byte & 0xF, byte >> 4)
 
 
-def find_ref_start(path: str, tid: int) -> int | None:
-    """Virtual offset of the first record whose refID is >= tid or -1 (None: the file ends
-    first), found without inflating the file (bcio_find_ref_start).  Exact for a file grouped by
-    reference; BamStream(voff_range=...) streams verify it (a wrong split fails their decode)."""
+def find_ref_start(path: str, tid: int, pos: int | None = None) -> int | None:
+    """Virtual offset of the first record whose refID is >= tid or -1 (with ``pos``: the first
+    at or past (tid, pos) in coordinate order), None if the file ends first; found without
+    inflating the file (bcio_find_ref_start / bcio_find_record).  Exact for a coordinate-sorted
+    file; BamStream(voff_range=...) streams verify a split (a wrong one fails their decode)."""
     lib = N.bcio()
     v = C.c_uint64()
-    rc = lib.bcio_find_ref_start(os.fsencode(path), int(tid), C.byref(v))
+    if pos is None:
+        rc = lib.bcio_find_ref_start(os.fsencode(path), int(tid), C.byref(v))
+    else:
+        rc = lib.bcio_find_record(os.fsencode(path), int(tid), int(pos), C.byref(v))
     if rc == -1:
         raise FileNotFoundError(lib.bcio_last_error().decode())
     N.bcio_check(rc)

@@ -211,6 +211,18 @@ int bc_gather_dev(bc_comm* c, const void* d_send, int64_t n, void* d_recv, const
     return BC_OK;
 }
 
+int bc_reduce_i32_dev(bc_comm* c, const int32_t* d_send, int32_t* d_recv, int64_t n, int root) {
+    if (!c || n < 0 || root < 0 || root >= c->world) return cfail(BC_E_ARG, "bad argument");
+    if (n > 0 && !d_send) return cfail(BC_E_ARG, "d_send is NULL");
+    if (c->rank == root && n > 0 && !d_recv) return cfail(BC_E_ARG, "d_recv is NULL on the root");
+    if (n == 0) return BC_OK;
+    Dev g(c->ctx->device);
+    // (the receive buffer is only written on the root; elsewhere RCCL takes the send buffer)
+    NCCL_TRY(ncclReduce(d_send, c->rank == root ? (void*)d_recv : (void*)d_send, (size_t)n, ncclInt32, ncclSum,
+                        root, c->nc, c->ctx->stream));
+    return BC_OK;
+}
+
 int bc_gather_bytes(bc_comm* c, const void* h_send, int64_t n, void* h_recv, const int64_t* sizes, int root) {
     if (!c || !sizes || n < 0 || (n > 0 && !h_send) || root < 0 || root >= c->world)
         return cfail(BC_E_ARG, "bad argument");

@@ -1064,8 +1064,10 @@ int header_span(const uint8_t* comp, uint64_t n, int32_t* n_ref, uint64_t* first
 
 }  // namespace
 
-extern "C" int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff) {
+extern "C" int bcio_find_record(const char* path, int32_t tid, int32_t pos, uint64_t* voff) {
     if (!path || !voff) return fail(BCIO_E_ARG, "null argument");
+    // the first record at or past (tid, pos): refID -1 (unmapped) sorts after every reference
+    auto past = [tid, pos](int32_t ref, int32_t rpos) { return ref < 0 || ref > tid || (ref == tid && rpos >= pos); };
     FileMap fm;
     const int orc = fm.open_as(path, FileMap::kRandom);  // a few probes: no readahead of the file
     if (orc == -1) return fail(BCIO_E_IO, std::string("cannot open ") + path);
@@ -1081,22 +1083,18 @@ extern "C" int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff
     // hi: a file offset such that the first record synchronised in any block at or after it has
     // refID >= tid (or -1); the bisection narrows [lo's block, hi) to a few blocks
     uint64_t hi = n;
-    auto ref_at = [&](uint64_t v, int32_t* ref, bool* end) -> int {  // refID of the record at v
+    {  // the first record itself
         Span sp;
-        sp.next = v >> 16;
-        const uint64_t u = v & 0xFFFF;
-        int rc2 = span_grow(comp, n, sp, u + 36);
-        if (rc2 != BCIO_OK) return rc2;
-        *end = sp.buf.size() <= u;
-        *ref = *end ? -1 : (sp.buf.size() >= u + 8 ? rd32s(sp.buf.data() + u + 4) : -2);
-        return *ref == -2 ? fail(BCIO_E_FORMAT, "truncated BAM record") : BCIO_OK;
-    };
-    {
-        int32_t r0 = 0;
-        bool end = false;
-        if ((rc = ref_at(first, &r0, &end)) != BCIO_OK) return rc;
-        if (tid <= 0 || end || r0 < 0 || r0 >= tid) {
-            *voff = end ? 0 : first;
+        sp.next = first >> 16;
+        const uint64_t u = first & 0xFFFF;
+        if ((rc = span_grow(comp, n, sp, u + 36)) != BCIO_OK) return rc;
+        if (sp.buf.size() <= u) {
+            *voff = 0;  // no records
+            return BCIO_OK;
+        }
+        if (sp.buf.size() < u + 12) return fail(BCIO_E_FORMAT, "truncated BAM record");
+        if (past(rd32s(sp.buf.data() + u + 4), rd32s(sp.buf.data() + u + 8))) {
+            *voff = first;
             return BCIO_OK;
         }
     }
@@ -1120,8 +1118,7 @@ extern "C" int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff
             hi = mid;
             continue;
         }
-        const int32_t ref = rd32s(sp.buf.data() + o + 4);
-        if (ref >= 0 && ref < tid) lo = std::max(lo, span_voff(sp, (uint64_t)o));
+        if (!past(rd32s(sp.buf.data() + o + 4), rd32s(sp.buf.data() + o + 8))) lo = std::max(lo, span_voff(sp, (uint64_t)o));
         else hi = (uint64_t)c;
     }
     // hop records from lo to the first with refID >= tid or -1 (or the end of the file)
@@ -1134,9 +1131,8 @@ extern "C" int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff
             *voff = 0;  // no such record: the range runs to the end of the file
             return BCIO_OK;
         }
-        if (u + 8 > sp.buf.size()) return fail(BCIO_E_FORMAT, "truncated BAM record");
-        const int32_t ref = rd32s(sp.buf.data() + u + 4);
-        if (ref < 0 || ref >= tid) {
+        if (u + 12 > sp.buf.size()) return fail(BCIO_E_FORMAT, "truncated BAM record");
+        if (past(rd32s(sp.buf.data() + u + 4), rd32s(sp.buf.data() + u + 8))) {
             *voff = span_voff(sp, u);
             return BCIO_OK;
         }
@@ -1154,6 +1150,10 @@ extern "C" int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff
             u -= cut;
         }
     }
+}
+
+extern "C" int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff) {
+    return bcio_find_record(path, tid, INT32_MIN, voff);
 }
 
 extern "C" int bcio_stream_open_range(const char* path, int nthreads, uint64_t voff_begin, uint64_t voff_end,

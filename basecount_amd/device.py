@@ -118,6 +118,7 @@ def lib() -> C.CDLL:
         "bc_gather_layout": ([vp, C.c_int, vp], C.c_int),
         "bc_gather_bytes": ([vp, vp, i64, vp, vp, C.c_int], C.c_int),
         "bc_gather_dev": ([vp, vp, i64, vp, vp, C.c_int], C.c_int),
+        "bc_reduce_i32_dev": ([vp, vp, vp, i64, C.c_int], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -194,6 +194,11 @@ class RcclGroup(_GroupOps):
         self.D.check(self.D.lib().bc_allgather_i64(self.h, a.ctypes.data, a.size, out.ctypes.data))
         return out.reshape(self.world, a.size).tolist()
 
+    def reduce_i32(self, buf, n: int, root: int) -> None:
+        """Sum every rank's int32 device buffer [n] into root's, in place (RCCL reduce on the
+        rank's stream, after the kernels that filled it)."""
+        self.D.check(self.D.lib().bc_reduce_i32_dev(self.h, buf.ptr, buf.ptr, int(n), int(root)))
+
     def broadcast_bytes(self, data: bytes) -> bytes:
         n = self.all_gather_ints([len(data)])[0][0]
         buf = (C.c_uint8 * max(1, n))()
@@ -260,6 +265,15 @@ class GlooGroup(_GroupOps):
         out = [self.torch.empty_like(t) for _ in range(self.world)]
         self.td.all_gather(out, t)
         return [o.tolist() for o in out]
+
+    def reduce_i32(self, buf, n: int, root: int) -> None:
+        """reduce_i32 through the host (gloo tests: several ranks share one GPU)."""
+        import numpy as np
+
+        t = self.torch.from_numpy(np.ascontiguousarray(buf.download(np.int32, int(n))))
+        self.td.reduce(t, dst=int(root), op=self.td.ReduceOp.SUM)
+        if self.rank == root:
+            buf.upload(t.numpy())
 
     def broadcast_bytes(self, data: bytes) -> bytes:
         n = self.all_gather_ints([len(data)])[0][0]
@@ -341,6 +355,41 @@ def shard_contiguous(weights: list, world: int) -> list[int]:
         cuts.insert(best + 1, m)
     cuts += [n] * (world + 1 - len(cuts))
     return cuts
+
+
+BOUND = -(2 ** 31)  # a cut at a reference's start (before any of its reads)
+
+
+def plan_ranges(lengths: list, wanted: list, world: int, split_max: int):
+    """The sharded decode's ranges: cut points [(refID, pos)] * (world + 1) of a coordinate-
+    sorted file, rank r holding the records in [cut[r], cut[r + 1]) (coordinate order; pos BOUND:
+    the reference's start; cut[world] = (n_refs, BOUND), the last rank also holds the unmapped
+    reads).  When every requested reference is at most `split_max` positions long (C2-C4-like
+    files), the requested references' concatenated positions are cut into `world` equal parts,
+    so one reference's reads can be split over ranks (their histograms are then summed into the
+    reference's owner); otherwise whole references (shard_contiguous).
+    Returns (cuts, owner_of_tid, split_tids)."""
+    n = len(lengths)
+    wl = [int(L) if w else 0 for L, w in zip(lengths, wanted)]
+    total = sum(wl)
+    if world > 1 and total > 0 and all(int(L) <= split_max for L, w in zip(lengths, wanted) if w):
+        cuts = [(0, BOUND)]
+        starts = [0]
+        for x in wl:
+            starts.append(starts[-1] + x)
+        for r in range(1, world):
+            x = total * r // world
+            t = next(u for u in range(n) if wl[u] > 0 and starts[u] <= x < starts[u + 1])
+            pos = x - starts[t]
+            cuts.append((t, BOUND) if pos == 0 else (t, pos))
+        cuts.append((n, BOUND))
+    else:
+        cuts = [(t, BOUND) for t in shard_contiguous(wl, world)]
+    split = {t for t, p in cuts[1:-1] if p != BOUND}
+    owner = {}
+    for t in range(n):
+        owner[t] = max(r for r in range(world) if cuts[r] <= (t, BOUND))
+    return cuts, owner, split
 
 
 def _stdout_bytes(data: bytes) -> None:

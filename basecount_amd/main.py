@@ -560,42 +560,49 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         owner = None
         mine = ref_order
         t_lo, t_hi = 0, len(names)  # the refIDs this rank's byte range holds (sharded decode)
+        split = set()  # references whose reads several ranks count (their histograms are summed)
         if sharded:
-            from .dist import shard_contiguous
+            from .dist import BOUND, plan_ranges
 
-            # contiguous refID runs per rank (file order), balanced on the requested references'
-            # lengths; each rank streams only the bytes from its first reference's first record
-            # to the next rank's (the last rank: to the end of the file, unmapped reads included)
-            cuts = shard_contiguous([int(stream.lengths[t]) if wanted_t else 0
-                                     for t, wanted_t in enumerate(n in references for n in names)], _group.world)
-            owner = {r: next(i for i in range(_group.world) if cuts[i] <= ref_index[r] < cuts[i + 1])
-                     for r in ref_order}
+            # contiguous coordinate ranges per rank (file order): whole references balanced on
+            # the requested lengths, or, when every requested reference is small (C2-C4-like),
+            # equal cuts of their positions, one reference's reads split over several ranks.
+            # Each rank streams only the bytes of its range (the last: to the end of the file,
+            # unmapped reads included)
+            cuts, owner_t, split_t = plan_ranges([int(x) for x in stream.lengths], wanted, _group.world,
+                                                 int(os.environ.get("BASECOUNT_SPLIT_MAX", str(1 << 22))))
+            owner = {r: owner_t[ref_index[r]] for r in ref_order}
+            split = {names[t] for t in split_t} & set(ref_order)
             mine = [r for r in ref_order if owner[r] == _group.rank]
-            t_lo, t_hi = cuts[_group.rank], cuts[_group.rank + 1]
-            last = _group.rank == _group.world - 1
+            rk = _group.rank
+            last = rk == _group.world - 1
+            t_lo = cuts[rk][0]
+            t_hi = len(names) if last else cuts[rk + 1][0] + (1 if cuts[rk + 1][1] != BOUND else 0)
+
+            def where(c):
+                return find_ref_start(bam, c[0]) if c[1] == BOUND else find_ref_start(bam, c[0], c[1])
+
             with _phase("decode"):
-                beg = find_ref_start(bam, t_lo)
-                end = None if last else find_ref_start(bam, t_hi)
+                beg = where(cuts[rk])
+                end = None if last else where(cuts[rk + 1])
                 if beg is None or (end is not None and end <= beg):
                     beg = end = None  # no records in this rank's range
                 stream.close()
                 stream = BamStream(bam, voff_range=(beg, end))
-            if last:
-                t_hi = len(names)
         elif _group is not None:
             from .dist import shard
 
             # cost estimate before any read is seen: the per-position outputs (linear in length)
             owner = shard(ref_order, {r: int(reference_lengths[r]) for r in ref_order}, _group.world)
             mine = [r for r in ref_order if owner[r] == _group.rank]
-        mine_t = {ref_index[r] for r in mine}
+        mine_t = {ref_index[r] for r in mine} | {ref_index[r] for r in split}  # the references counted here
         B = batch_records(chunk_size)
         fl = _Faults()
         nreads = {ref: 0 for ref in ref_order}
         results = {}
         acc = {}  # ref -> device histogram accumulating its batches (int32 [ncols][L])
         finished = set()
-        ctx = context(device) if (mbq_ok and mine) else None
+        ctx = context(device) if (mbq_ok and (mine or split)) else None
         scratch = _scratch(ctx) if ctx is not None else None
         nf, nf2 = norm_factors(k)
 
@@ -605,6 +612,7 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         base = 0  # accepted reads before the current batch (global ordinals; sharded: in the range)
         cur = nxt = None
         miss = False
+        split_acc = {}  # split reference -> this rank's histogram of its reads
 
         def next_batch():
             if not sharded:
@@ -664,7 +672,9 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                     for ref in here:
                         t = ref_index[ref]
                         L = int(reference_lengths[ref])
-                        closed = grouped and (nxt is None or int(nsel.ref_beg[t + 1]) == int(nsel.ref_beg[t]))
+                        # (a reference split over ranks is never complete on one: accumulated)
+                        closed = grouped and ref not in split and (
+                            nxt is None or int(nsel.ref_beg[t + 1]) == int(nsel.ref_beg[t]))
                         reads = _indexed(ctx, bod.reads(t), L, scratch)
                         b0 = int(sel.ref_beg[t])
                         if closed and ref not in acc:  # the whole reference in this batch: fused
@@ -691,9 +701,12 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 base += sel.n_accepted
                 cur.close()
                 cur, nxt = nxt, None
+            for ref in split:  # summed over the ranks once every rank is done (below)
+                if ref in acc:
+                    split_acc[ref] = acc.pop(ref)
             if ctx is not None and fl.inloop() is None:
                 for ref in mine:
-                    if ref in results:
+                    if ref in results or ref in split:
                         continue
                     L = int(reference_lengths[ref])
                     if ref in acc:
@@ -713,7 +726,9 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
             for b in acc.values():
                 b.free()
         if sharded:
-            if not _merge_shards(_group, fl, miss, base, ref_order, owner, names, nreads):
+            if not _merge_shards(_group, fl, miss, base, ref_order, names, nreads):
+                for b in split_acc.values():
+                    b.free()
                 return None  # some rank's range did not confirm: every rank decodes the file
         elif _group is not None and mbq_ok:
             # every rank needs every reference's first out-of-range read to raise the same error
@@ -724,10 +739,32 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 o, bp = alls[owner[r]][2 * i], alls[owner[r]][2 * i + 1]
                 if o >= 0:
                     fl.range_[r] = (o, bp)
-        err = _first_error(fl, ref_order, reference_lengths, mbq, int(chunk_size),
-                           _type_args(bam, B, mmq, wanted, ref_index))
-        if err is not None:
-            raise err
+        try:
+            err = _first_error(fl, ref_order, reference_lengths, mbq, int(chunk_size),
+                               _type_args(bam, B, mmq, wanted, ref_index))
+            if err is not None:
+                raise err
+            # split references: every rank's histogram summed into the owner's (RCCL reduce over
+            # xGMI, in rank 0's reference order on every rank), then kernel 2 on the owner
+            for ref in ref_order:
+                if ref not in split or ctx is None:
+                    continue
+                L = int(reference_lengths[ref])
+                buf = split_acc.pop(ref, None)
+                if buf is None:
+                    buf = ctx.alloc(max(16, 4 * ncols * L))
+                    buf.zero()
+                with _phase("reduce"):
+                    _group.reduce_i32(buf, ncols * L, owner[ref])
+                if owner[ref] == _group.rank:
+                    results[ref] = _finish_reference(ctx, buf, L, ncols, k, nf, nf2, _mode, tiles_of(ref),
+                                                     _tiles is not None, scratch)
+                else:
+                    ctx.sync()
+                    buf.free()
+        finally:
+            for b in split_acc.values():
+                b.free()
         out = {}
         for ref in mine:
             n = nreads[ref]
@@ -743,7 +780,7 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         stream.close()
 
 
-def _merge_shards(group, fl: _Faults, miss: bool, n_accepted: int, ref_order, owner, names, nreads) -> bool:
+def _merge_shards(group, fl: _Faults, miss: bool, n_accepted: int, ref_order, names, nreads) -> bool:
     """Sharded decode: turn this rank's range-local fault ordinals into the file's (each range
     starts after the accepted reads of the ranges before it) and give every rank the faults the
     whole file holds, as one process streaming it would have recorded them.  False (on every rank)
@@ -774,16 +811,19 @@ def _merge_shards(group, fl: _Faults, miss: bool, n_accepted: int, ref_order, ow
             fl.keyerror = (b + v[4], names[v[5]] if v[5] >= 0 else None)
         if v[6] >= 0 and fl.clip is None:
             fl.clip = b + v[6]
+    # a reference's reads lie in its owner's range, or, split over ranks, in several: the first
+    # fault is the smallest file ordinal over them, the read count their sum
     for j, r in enumerate(ref_order):
-        i = owner[r]
-        v = alls[i]
-        nreads[r] = v[7 + 4 * j + 3]
-        if i > cut:
-            continue
-        if v[7 + 4 * j] >= 0:
-            fl.type_ord[r] = bases[i] + v[7 + 4 * j]
-        if v[7 + 4 * j + 1] >= 0:
-            fl.range_[r] = (bases[i] + v[7 + 4 * j + 1], v[7 + 4 * j + 2])
+        nreads[r] = sum(v[7 + 4 * j + 3] for v in alls)
+        for i in range(cut + 1):
+            v = alls[i]
+            if v[7 + 4 * j] >= 0:
+                o = bases[i] + v[7 + 4 * j]
+                fl.type_ord[r] = min(fl.type_ord.get(r, o), o)
+            if v[7 + 4 * j + 1] >= 0:
+                o = bases[i] + v[7 + 4 * j + 1]
+                if r not in fl.range_ or o < fl.range_[r][0]:
+                    fl.range_[r] = (o, v[7 + 4 * j + 2])
     return True
 
 

@@ -349,6 +349,10 @@ int bc_gather_layout(const int64_t* sizes, int world, int64_t* offsets /* [world
  *   bc_gather_dev:   device buffers, stream-ordered on the context's stream, capturable.       */
 int bc_gather_bytes(bc_comm* comm, const void* h_send, int64_t n, void* h_recv, const int64_t* sizes, int root);
 int bc_gather_dev(bc_comm* comm, const void* d_send, int64_t n, void* d_recv, const int64_t* sizes, int root);
+/* One reference's reads split over the ranks (a single contig on N GPUs): every
+ * rank's int32 histogram [n] summed into root's d_recv (may alias d_send; ignored off the root).
+ * Device buffers, stream-ordered on the context's stream, capturable (RCCL reduce over xGMI). */
+int bc_reduce_i32_dev(bc_comm* comm, const int32_t* d_send, int32_t* d_recv, int64_t n, int root);
 
 /* Drop-in for count.bcount with host buffers: uploads, counts all 6 columns, downloads.
  * h_out: refLen x 6 uint32, ROW-major like the reference's vector<vector<unsigned>>

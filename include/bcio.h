@@ -133,6 +133,9 @@ void bcio_stream_close(bcio_stream* s);
  * voff_begin must be a record start.  If the record chain does not end exactly at voff_end,
  * bcio_stream_next fails with BCIO_E_FORMAT ("truncated BAM record"): the split was wrong. */
 int bcio_find_ref_start(const char* path, int32_t tid, uint64_t* voff);
+/* The same for the first record at or past (tid, pos) in coordinate order (refID tid and
+ * position >= pos, or a later refID, or -1): a split point inside one reference's reads. */
+int bcio_find_record(const char* path, int32_t tid, int32_t pos, uint64_t* voff);
 int bcio_stream_open_range(const char* path, int nthreads, uint64_t voff_begin, uint64_t voff_end,
                            bcio_stream** out);
 

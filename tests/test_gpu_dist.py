@@ -84,6 +84,11 @@ def test_rccl_group_world1(monkeypatch):
         # a wrong own size is an argument error, not a hang
         bad = np.array([8], np.int64)
         assert D.lib().bc_gather_dev(g.h, src.ptr, 64, dst.ptr, bad.ctypes.data, 0) == D.BC_E_ARG
+        # the split-reference histogram sum (RCCL reduce; the identity at world 1), in place
+        h = ctx.alloc(4 * 1000).upload(np.arange(1000, dtype=np.int32))
+        g.reduce_i32(h, 1000, 0)
+        assert np.array_equal(h.download(np.int32, 1000), np.arange(1000, dtype=np.int32))
+        assert D.lib().bc_reduce_i32_dev(g.h, h.ptr, h.ptr, 1000, 1) == D.BC_E_ARG  # no rank 1
     finally:
         g.close()
 
@@ -224,3 +229,46 @@ def test_sharded_decode_halves_the_c5_decode(tmp_path):
         best2.append(max(decode_ms(e) for e in err2))
     print(f"C5 decode: one rank {min(best1):.1f} ms, two ranks (slower) {min(best2):.1f} ms")
     assert min(best2) < 0.75 * min(best1), (best1, best2)
+
+
+@pytest.fixture(scope="module")
+def single_contig_bams(tmp_path_factory):
+    """One 29,903-bp contig (C2/C3-like), mixed CIGARs: its reads are split over the ranks."""
+    from basecount_amd import synth
+
+    d = tmp_path_factory.mktemp("split")
+    rs = synth.make_reads([("MN908947.3", 29_903)], 40_000, True, 23)
+    ok = str(d / "one.bam")
+    synth.write_bam(rs, ok)
+    # a read in the middle of the file (a later rank's range) runs past the end: the file stays
+    # sorted if it is the last read (so the error comes from the last rank)
+    rs.pos[-1] = 29_903 - 20
+    bad = str(d / "one_range_error.bam")
+    synth.write_bam(rs, bad)
+    two = synth.make_reads([("a", 20_000), ("b", 9_000)], 15_000, True, 24)
+    pair = str(d / "two.bam")
+    synth.write_bam(two, pair)
+    return ok, bad, pair
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_reference_cli_matches_one_process(single_contig_bams, tmp_path, world):
+    """a single contig's reads split over the ranks by position, each rank counting
+    its byte range of the file, the histograms summed into the owner (reduce), kernel 2 there.
+    Rows, long format, summaries and the range error identical to one process."""
+    ok, bad, pair = single_contig_bams
+    cases = [(ok, []), (ok, ["--long-format", "--show-n-bases", "--min-base-quality", "20"]),
+             (ok, ["--summarise"]), (pair, ["--summarise", "--min-mapping-quality", "30"]), (pair, []),
+             (bad, [])]
+    for i, (bam, args) in enumerate(cases):
+        rc1, out1, err1 = _ranks(1, [bam, *args], tmp_path, f"s{i}")
+        env = {"BASECOUNT_SHARD_DECODE": "require", "BASECOUNT_HIP_TIMING": "1"}
+        rcn, outn, errn = _ranks(world, [bam, *args], tmp_path, f"m{i}", env)
+        if rc1[0] == 0:
+            assert rcn == [0] * world, (args, [e[-1500:] for e in errn])
+            assert outn == out1, args
+            assert any("host reduce" in e for e in errn), "no histogram was reduced"
+        else:
+            assert all(r != 0 for r in rcn), (args, rcn)
+            assert _last_line(errn[0]) == _last_line(err1[0]), (args, errn[0][-800:])

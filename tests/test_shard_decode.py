@@ -156,3 +156,50 @@ def test_shard_contiguous_balances_grch38():
         loads = [sum(L[c[i]:c[i + 1]]) for i in range(world)]
         assert c[0] == 0 and c[-1] == len(L) and all(a <= b for a, b in zip(c, c[1:]))
         assert max(loads) <= 1.25 * sum(L) / world + max(L)
+
+
+def test_find_record_inside_a_reference(tmp_path):
+    """bcio_find_record: the first record at or past (tid, pos) splits one reference's reads."""
+    rs = synth.make_reads([("one", 29_903)], 60_000, True, 15)
+    p = str(tmp_path / "one.bam")
+    synth.write_bam(rs, p)
+    tid, pos, _, _ = _whole(p)
+    for q in (1, 7_475, 14_951, 22_427, 29_000, 40_000):
+        v = find_ref_start(p, 0, q)
+        k = int(np.count_nonzero(pos < q))  # the file is sorted: the first k records come before
+        if k == tid.size:
+            assert v is None
+            continue
+        with BamStream(p, voff_range=(v, None)) as s:
+            n = sum(b.n_records for b in s.batches(1 << 20))
+        assert n == tid.size - k, q
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_plan_ranges_split_one_reference(tmp_path, world):
+    """Every requested reference small: their positions are cut into equal parts, the ranges
+    partition the file and each holds a share of the reads."""
+    from basecount_amd.dist import BOUND, plan_ranges
+
+    rs = synth.make_reads([("one", 29_903)], 30_000, False, 16)
+    p = str(tmp_path / "one.bam")
+    synth.write_bam(rs, p)
+    cuts, owner, split = plan_ranges([29_903], [True], world, 1 << 22)
+    assert split == {0} and owner == {0: 0} and len(cuts) == world + 1
+    counts = []
+    for r in range(world):
+        beg = find_ref_start(p, *cuts[r]) if cuts[r][1] != BOUND else find_ref_start(p, cuts[r][0])
+        end = None if r == world - 1 else find_ref_start(p, *cuts[r + 1])
+        with BamStream(p, voff_range=(beg, end)) as s:
+            counts.append(sum(b.n_records for b in s.batches(1 << 20)))
+    assert sum(counts) == rs.n
+    assert min(counts) > 0.5 * rs.n / world
+
+
+def test_plan_ranges_whole_references_when_large():
+    from basecount_amd.dist import BOUND, plan_ranges
+
+    L = [x for _, x in synth.GRCH38]
+    cuts, owner, split = plan_ranges(L, [True] * len(L), 8, 1 << 22)
+    assert not split and all(p == BOUND for _, p in cuts)
+    assert [owner[t] for t in range(len(L))] == sorted(owner[t] for t in range(len(L)))

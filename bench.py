@@ -700,6 +700,89 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     return res
 
 
+def run_split(ctx, group, steps: int, warmup: int) -> dict:
+    """C3 on N ranks with its one contig's reads split N ways (a single contig on
+    several GPUs): each rank counts a contiguous slice of the sorted batch (k_rc into its own
+    histogram, zeroed per step), an RCCL reduce (bc_reduce_i32_dev, 5 x 29,903 int32) sums the
+    histograms into rank 0, which runs kernel 2.  Strong scaling: every step is the whole C3 job;
+    `value` = the contig's positions per second.  Gloo rehearsals reduce through the host."""
+    import oracle as O
+    from basecount_amd import device as D
+    from basecount_amd import synth
+    from basecount_amd.bam import seq_to_event
+    from basecount_amd.main import norm_factors
+
+    rank, world = group.rank, group.world
+    rs = synth.make_config("c3")
+    b = synth.batch_arrays(rs, 0, 0)
+    L, k = rs.lengths[0], 5
+    nf, nf2 = norm_factors(k)
+    n = int(b["pos"].size)
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    mine = dict(b, qual=None, seq_event=seq_to_event(b["seq"]),
+                **{f: b[f][lo:hi] for f in ("pos", "cig_beg", "cig_n", "seq_nib")})
+    reads = D.DeviceReads(ctx, mine)
+    hist = ctx.alloc(4 * k * L)
+    outs = {name: ctx.alloc(nb) for name, nb in (("cov", 4 * L), ("ent", 8 * L), ("sec", 8 * L))}
+    rccl = getattr(group, "backend", "") == "rccl"
+
+    def step():
+        hist.zero()
+        ctx.count(reads.r, L, 0, k, hist.ptr)
+        group.reduce_i32(hist, k * L, 0)
+        if rank == 0:
+            ctx.stats(hist.ptr, L, k, nf, nf2, outs["cov"].ptr, None, outs["ent"].ptr, outs["sec"].ptr)
+
+    for _ in range(warmup):
+        step()
+    ctx.sync()
+    group.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.sync()
+    group.barrier()
+    elapsed = max_over_ranks(group, time.perf_counter() - t0)
+    # a step's parts on this rank: k_rc on the slice, the reduce (RCCL: on the stream)
+    ctx.timing(True)
+    step()
+    rep = ctx.timing_report()
+    ctx.timing(False)
+    ctx.sync()
+    if rccl:
+        ctx.event_record(2)
+        for _ in range(20):
+            group.reduce_i32(hist, k * L, 0)
+        ctx.event_record(3)
+        reduce_us = ctx.event_elapsed_ms(2, 3) * 1e3 / 20
+    else:
+        reduce_us = None
+    step()  # the counts of one step, reduced at rank 0
+    ctx.sync()
+    ok = True
+    if rank == 0:
+        exp, _ = O.bcount(L, 0, b, nthreads=cpu_threads())
+        got = hist.download(np.int32, k * L).reshape(k, L)
+        ok = bool(np.array_equal(got, exp[:, :k].T.astype(np.int32)))
+        _, _, oent, _ = O.stats(exp, False, nthreads=cpu_threads())
+        ok = ok and float(np.max(np.abs(outs["ent"].download(np.float64, L) - oent))) <= 1e-6
+    ok = all(v[0] == 1 for v in group.all_gather_ints([int(ok)]))
+    reads.free()
+    hist.free()
+    for v in outs.values():
+        v.free()
+    return {
+        "workload": "C3's contig (29,903 bp, 1,000,000 mixed-CIGAR reads) split over the ranks by read: "
+                    "k_rc per slice + reduce to rank 0 + k_stats",
+        "value": L * steps / elapsed, "unit": "positions/s", "ms_per_step": elapsed / steps * 1e3,
+        "scaling": "strong", "n_gpus": world, "reads_per_rank": hi - lo,
+        "kernel_us": {KERNEL_NAMES[nm]: v[1] for nm, v in rep.items() if nm in KERNEL_NAMES},
+        "reduce_us": reduce_us, "reduce_bytes": 4 * k * L, "comm": getattr(group, "backend", "?"),
+        "parity_vs_oracle": ok,
+    }
+
+
 def run_unsorted(ctx, args, reps: int = 20) -> dict:
     """C3's reads in random order (an unsorted BAM's batch, main.py:127 consumes file order):
     the event-parallel k_count (+ k_stats) path against the device sort (bc_reads_sort: counting
@@ -946,6 +1029,8 @@ def main():
             extra[cfg] = r
         if world == 1:
             extra["c3_unsorted"] = run_unsorted(ctx, args)
+        else:  # one contig over the ranks: its reads split, histograms reduced to rank 0
+            extra["c3_split"] = run_split(ctx, group, min(args.steps, 100), min(args.warmup, 10))
 
     cpu = cpu_all = e2e_res = None
     if rank == 0 and world == 1:

@@ -130,6 +130,8 @@ def test_bench_gpus_2_rehearsal():
     assert d["n_gpus"] == 2 and d["config"]["comm"] == "gloo" and d["parity_vs_oracle"]
     c5 = d["extra"]["c5"]
     assert c5["parity_vs_oracle"] and c5["gather_bytes"] == 32 * 24 and c5["scaling"] == "strong"
+    sp = d["extra"]["c3_split"]  # C3's one contig split over the two ranks, histograms reduced
+    assert sp["parity_vs_oracle"] and sp["reads_per_rank"] == 500_000 and sp["scaling"] == "strong"
 
 
 # ------------------------------------------------------------------ sharded decode

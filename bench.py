@@ -503,14 +503,30 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         if gather is not None:
             gather_step()
 
+    # Consecutive steps are independent batches: with --pipeline 2 (the default for the one-stream
+    # configs) the K timed steps run two in flight, alternating between two contexts (own scratch
+    # and outputs; fork / join inside the one captured graph), so a step's tail overlaps the next
+    # step's head as a stream of batches runs.  Every step still does all of its work; the
+    # serialized step time is reported beside it (serial_us_per_step).
+    pipe = (args.pipeline == 2 and launch == "graph" and gather is None and not summarise
+            and len(wl.ctxs) == 1 and not args.lean)
+    side = None
+    if pipe:
+        from basecount_amd import device as Dm
+
+        side = Dm.Context(ctx.device)
+        side.set_shape(args.shape, args.tile_waves)
     for _ in range(warmup):
         step()
+    if pipe:
+        wl.pipelined(max(2, warmup), side)  # (also allocates the side context's scratch, uncaptured)
+        side.sync()
     ctx.sync()
-    if ctx.range_error() != -1:
+    if ctx.range_error() != -1 or (side is not None and side.range_error() != -1):
         raise RuntimeError(f"{cfg}: out-of-range event in a synthetic batch")
     graph = None
     if launch == "graph" and gather is None:  # the same K steps, replayed from one captured graph
-        graph = ctx.capture(lambda: [step() for _ in range(steps)])
+        graph = ctx.capture((lambda: wl.pipelined(steps, side)) if pipe else (lambda: [step() for _ in range(steps)]))
         graph.launch()  # untimed replay (first-launch setup)
         ctx.sync()
     if group is not None:
@@ -597,24 +613,18 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         ctx.event_record(3)
         extra_us["raw_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
         del g
-    if not summarise and group is None and len(wl.ctxs) == 1 and not args.lean:
-        # two steps in flight on two streams (consecutive batches of a stream overlap): reported
-        # beside the serialized step, never as `value`
-        from basecount_amd import device as Dm
-
-        side = Dm.Context(ctx.device)
-        side.set_shape(args.shape, args.tile_waves)
-        wl.pipelined(4, side)  # first use: the side context's scratch is allocated outside the capture
-        ctx.sync()
-        side.sync()
-        g = ctx.capture(lambda: wl.pipelined(steps, side))
+    if pipe:
+        # the same K steps serialized on one stream, one graph: the step's own latency
+        g = ctx.capture(lambda: [step() for _ in range(steps)])
         g.launch()
         ctx.sync()
         ctx.event_record(2)
         g.launch()
         ctx.event_record(3)
-        extra_us["pipelined_2_streams_us_per_step"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        extra_us["serial_us_per_step"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
         del g
+    if side is not None:
+        side.sync()
         side.close()
     gather_us = None
     if gather is not None:
@@ -671,7 +681,9 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                    + (", + numpy-exact summary per contig" if summarise else "")
                    + (", + RCCL gather of the summaries to rank 0" if gather is not None else "")
                    + (", the K timed steps replayed from one hipGraph" if launch == "graph" and gather is None
-                      else ", eager launches"),
+                      else ", eager launches")
+                   + (", two steps in flight (two streams, alternating)" if pipe else ""),
+        "steps_in_flight": 2 if pipe else 1,
         "reads_per_rank": int(sum(int(w[2]["pos"].size) for w in wl.work)),
         "positions_per_rank": int(sum(w[1] for w in wl.work)),
         "contigs_per_rank": len(wl.work),
@@ -948,6 +960,9 @@ def main():
                     help="c5: contexts (streams) the contigs run on concurrently (bc_ctx_wait fork/join)")
     ap.add_argument("--read-runs", choices=["on", "off"], default="on",
                     help="off: drop the upload's run records (bc_reads.read_runs), A/B only")
+    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=2,
+                    help="steps in flight in the timed graph (2: consecutive batches overlap on two "
+                         "streams; 1: serialized)")
     ap.add_argument("--rotate", type=int, default=0,
                     help="device copies of each batch the steps rotate over (0: 3 for c3, whose 110 MB "
                          "would otherwise stay in the 256 MB Infinity Cache, else 1)")
@@ -1087,8 +1102,9 @@ def main():
         }
         if "gather_us" in head:
             line["gather_us"] = head["gather_us"]
-        if "pipelined_2_streams_us_per_step" in head:
-            line["pipelined_2_streams_us_per_step"] = head["pipelined_2_streams_us_per_step"]
+        line["steps_in_flight"] = head["steps_in_flight"]
+        if "serial_us_per_step" in head:
+            line["serial_us_per_step"] = head["serial_us_per_step"]
         if cpu:
             line["speedup_vs_cpu"] = head["value"] / cpu["value"]
             line["speedup_vs_cpu_all_cores"] = head["value"] / cpu_all["value"]

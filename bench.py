@@ -1044,6 +1044,18 @@ def main():
             extra[cfg] = r
         if world == 1:
             extra["c3_unsorted"] = run_unsorted(ctx, args)
+            if args.mbq == 0 and args.config != "c3":
+                # SURVEY §8(d) measures C3 at mbq/mmq 0/0 and 20/30: the quality test (mbq 20) adds
+                # the QUAL bytes to kernel 1's input (the mapq filter is the host's, before upload)
+                import argparse as _ap
+
+                aq = _ap.Namespace(**vars(args))
+                aq.mbq = 20
+                r = run_config("c3", ctx, group, aq, rank, world, min(args.steps, 200), min(args.warmup, 20),
+                               args.launch, summarise=False)
+                r.pop("_wl").free()
+                r["min_base_quality"] = 20
+                extra["c3_q20"] = r
         else:  # one contig over the ranks: its reads split, histograms reduced to rank 0
             extra["c3_split"] = run_split(ctx, group, min(args.steps, 100), min(args.warmup, 10))
 

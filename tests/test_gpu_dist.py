@@ -262,7 +262,8 @@ def test_split_reference_cli_matches_one_process(single_contig_bams, tmp_path, w
     ok, bad, pair = single_contig_bams
     cases = [(ok, []), (ok, ["--long-format", "--show-n-bases", "--min-base-quality", "20"]),
              (ok, ["--summarise"]), (pair, ["--summarise", "--min-mapping-quality", "30"]), (pair, []),
-             (bad, [])]
+             (pair, ["--references", "a"]),  # KeyError: 'b' (its reads fall in another rank's range)
+             (pair, ["--chunk-size", "2000"]), (bad, [])]
     for i, (bam, args) in enumerate(cases):
         rc1, out1, err1 = _ranks(1, [bam, *args], tmp_path, f"s{i}")
         env = {"BASECOUNT_SHARD_DECODE": "require", "BASECOUNT_HIP_TIMING": "1"}

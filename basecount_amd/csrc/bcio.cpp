@@ -34,6 +34,7 @@
 
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -89,6 +90,18 @@ inline void wr32(std::string& s, uint32_t v) {
     for (int i = 0; i < 4; ++i) s.push_back((char)((v >> (8 * i)) & 0xff));
 }
 
+// munmap in 16 MiB pieces: one munmap of a GB-sized range holds the process's mmap lock for tens
+// of ms, stalling every page fault and allocation of the other threads (the formatter right after
+// a batch is released, say); in pieces they interleave.
+inline void unmap_gradually(void* p, size_t n) {
+    constexpr size_t kPiece = 16u << 20;
+    uint8_t* b = (uint8_t*)p;
+    for (size_t off = 0; off < n; off += kPiece) {
+        munmap(b + off, std::min(kPiece, n - off));
+        if (off + kPiece < n) sched_yield();
+    }
+}
+
 // Anonymous mapping for the inflate buffer: no zero fill pass, hugepages where the kernel allows.
 class MapBuf {
 public:
@@ -106,7 +119,7 @@ public:
     uint8_t* data() { return p_; }
     size_t size() const { return n_; }
     void release() {
-        if (p_) munmap(p_, n_);
+        if (p_) unmap_gradually(p_, n_);
         p_ = nullptr;
     }
 
@@ -153,7 +166,7 @@ public:
     }
     ~FileMap() { release(); }
     void release() {
-        if (map_) munmap((void*)map_, n_);
+        if (map_) unmap_gradually((void*)map_, n_);
         map_ = nullptr;
         buf_.clear();
         buf_.shrink_to_fit();
@@ -191,6 +204,21 @@ struct UninitAlloc : std::allocator<T> {
     template <class U, class... A>
     void construct(U* p, A&&... a) {
         ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+    // large arrays (a batch's sequence, qualities, CIGARs) straight from mmap, given back in
+    // pieces (unmap_gradually) when the batch is released
+    static constexpr size_t kBig = 4u << 20;
+    T* allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < kBig) return std::allocator<T>::allocate(n);
+        void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (m == MAP_FAILED) throw std::bad_alloc();
+        return (T*)m;
+    }
+    void deallocate(T* p, size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < kBig) std::allocator<T>::deallocate(p, n);
+        else unmap_gradually(p, bytes);
     }
 };
 template <class T>

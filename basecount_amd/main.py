@@ -486,6 +486,19 @@ def batch_records(chunk_size: int) -> int:
     return min(max(cs, 1 << 16), 1 << 24) if cs > 0 else 1 << 22
 
 
+# Host buffers released at the end of the CLI run instead of when the stream ends: giving back a
+# GB of decoded batch and inflate buffers (munmap, TLB shootdowns on every core the process runs
+# on) right before the formatter stalled its threads by ~65 ms at C3.  None: release at once.
+_DEFERRED: list | None = None
+
+
+def _release(h) -> None:
+    if _DEFERRED is not None:
+        _DEFERRED.append(h)
+    else:
+        h.close()
+
+
 class _Ungrouped(Exception):
     """A reference's reads came back after the reference was finished (the file is not grouped
     by reference): start again, accumulating every reference until the end of the file."""
@@ -699,7 +712,10 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                     with _phase("device (sync)"):
                         ctx.sync()  # the batch's host arrays may go once its copies are done
                 base += sel.n_accepted
-                cur.close()
+                if nxt is None:
+                    _release(cur)  # the last batch: released after the output (CLI)
+                else:
+                    cur.close()
                 cur, nxt = nxt, None
             for ref in split:  # summed over the ranks once every rank is done (below)
                 if ref in acc:
@@ -777,7 +793,7 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
             return out, owner, ref_order
         return out
     finally:
-        stream.close()
+        _release(stream)
 
 
 def _merge_shards(group, fl: _Faults, miss: bool, n_accepted: int, ref_order, names, nreads) -> bool:
@@ -842,9 +858,10 @@ def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
         nb = ctx.sort_bytes(reads)
         reads = ctx.sort(reads, scratch.get("sorted", nb).ptr, nb)
     # the tile index only: a batch counted once does not recover the run records' build (C3:
-    # k_index_runs ~18 us against ~10 us saved in k_rc; bench.py reports both)
+    # k_index_runs ~18 us against ~10 us saved in k_rc; bench.py reports both), and none for a
+    # slice the read-chunked kernel takes (what BC_INDEX_AUTO would build is not the tiles)
     nb = ctx.index_bytes(reads, L, D.BC_INDEX_TILES)
-    if nb:
+    if nb and ctx.index_bytes(reads, L, D.BC_INDEX_AUTO) == nb:
         ctx.index(reads, L, scratch.get("index", nb).ptr, nb, D.BC_INDEX_TILES)
     return reads
 
@@ -1128,10 +1145,15 @@ def run(argv=None):
 
         t0 = time.perf_counter()
         context().timing(True)
+    global _DEFERRED
+    _DEFERRED = []
     try:
         _run(args, references, min_base_quality, min_mapping_quality, chunk_size, bed,
              decimal_places, group)
     finally:
+        deferred, _DEFERRED = _DEFERRED, None
+        for h in deferred:
+            h.close()
         if group is not None:
             group.close()
         if timing:

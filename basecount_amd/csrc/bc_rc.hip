@@ -73,6 +73,14 @@ __device__ __forceinline__ unsigned long long shl64_mod64(unsigned long long k, 
     return r;
 }
 
+// X >> n as ONE v_lshrrev_b64 (the compiler splits a 64-bit shift into two 32-bit funnel ops)
+template <int N>
+__device__ __forceinline__ unsigned long long shr64(unsigned long long x) {
+    unsigned long long r;
+    asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
+    return r;
+}
+
 struct RcArgs {
     const int32_t* pos;
     const uint32_t* cig_beg;
@@ -92,7 +100,8 @@ struct RcArgs {
     int32_t* counts;  // [ncols][L], accumulated into
     unsigned long long* err;
     int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events,
-                 // 512 no staging, 2048 no flush, 8192 no event image, 16384 no image expansion
+                 // 512 no staging, 2048 no flush, 8192 no event image, 16384 no image expansion,
+                 // 65536 no boundary rows in the image expansion
     unsigned long long* trace;  // diagnostic only (BC_PHASE_TRACE builds): [block][wave][kRcPhases]
 };
 
@@ -191,7 +200,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // the expansion (lanes = reads, one row) and the accumulation (lanes = rows, one read) hit
     // 64 different LDS banks
     constexpr int kRecU4 = kRcReads * 3, kImgU4 = kImgRows * kRcReads / 4;
-    __shared__ uint4 rec[kRecU4 > kImgU4 ? kRecU4 : kImgU4];
+    // the image's 32-read groups are R words apart beyond their 736 (R = the chunk's rows, <= 23),
+    // so the sum's lanes (row t mod R of group t / R) read 32 consecutive banks
+    constexpr int kImgPadU4 = (7 * kImgRows + 3) / 4;
+    __shared__ uint4 rec[kRecU4 > kImgU4 + kImgPadU4 ? kRecU4 : kImgU4 + kImgPadU4];
     uint32_t* img = (uint32_t*)rec;
     __shared__ int32_t rpos[kRcReads];  // the chunk's read positions (window tables)
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 8 * kPadW];  // + pads
@@ -389,6 +401,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const int64_t WBc = P0 & ~(int64_t)7;
         const int NWc = (int)(P1 > WBc ? (P1 - WBc + 7) / 8 : 0);
         const bool img_path = staged && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
+        const int gpad = NWc;  // (uniform) the image's group padding (see rec)
+        uint32_t* const mycol = img + tid * kImgRows + (tid >> 5) * gpad;  // this read's image column
         if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
             stage_wait();
             __syncthreads();
@@ -508,7 +522,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                             x &= ~bmask;
                         }
                     }
-                    img[tid * kImgRows + row] = x;
+                    mycol[row] = x;
                 }
             };
             // Interior rows, then boundary rows.  A row that no boundary (Z, B0, A1, SP) falls
@@ -532,34 +546,46 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)o1, row, 1);
                     const uint32_t x1 = __builtin_amdgcn_alignbit(n1, p1, sh1) & m1;
                     // (s0 & m0) | x1: a row lies in at most one segment
-                    img[tid * kImgRows + row] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n0, p0, sh0), m0, x1, 0xEA);
+                    mycol[row] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n0, p0, sh0), m0, x1, 0xEA);
                     p0 = n0;
                     p1 = n1;
                 }
                 // rows lying entirely in a deletion (>= 8 deleted positions; none in most waves)
-                for (uint32_t od = rowmask(B0e, A1); od; od &= od - 1u) img[tid * kImgRows + __builtin_ctz(od)] = kClsDel;
-                auto fix = [&](int b) {  // the row boundary b cuts, exactly
-                    const int rb = b >> 5;
-                    if ((b & 31) == 0 || rb >= kImgRows) return;
-                    const int lo = 32 * rb;
-                    auto ge = [&](int Y) {
-                        const int d = Y - lo;
-                        return (uint32_t)shl64_mod64(0xFFFFFFFFull, d < 0 ? 0 : (d > 32 ? 32 : d));
-                    };
-                    const uint32_t gz = ge(Z), gb = ge(B0e), ga = ge(A1), gs = ge(SP);
-                    const uint32_t x0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(w0[rb + 1], w0[rb], sh0), gz, gb, 0x40);
-                    const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(w1[rb + 1], w1[rb], sh1), ga, gs, 0x40);
-                    img[tid * kImgRows + rb] =
-                        __builtin_amdgcn_bitop3_b32(x0, x1, __builtin_amdgcn_bitop3_b32(kClsDel, gb, ga, 0x40), 0xFE);
-                };
-                fix(Z);
-                fix(B0e);
-                fix(A1);
-                fix(SP);
+                for (uint32_t od = rowmask(B0e, A1); od; od &= od - 1u) mycol[__builtin_ctz(od)] = kClsDel;
+                // The <= 4 rows the boundaries cut, rewritten with the exact formula, without
+                // branches: all 8 stage-word pairs are read before any is used (one LDS round
+                // trip, not two per boundary), and a boundary that cuts no row (b % 32 == 0) or
+                // lies past the image rewrites a row the formula gets right anyway (row 22 at
+                // most: its words are inside the stage pads).
+                if (!(BC_ABL(A) & 65536)) {  // (diagnostic 65536: no boundary rows)
+                    const int bs[4] = {Z, B0e, A1, SP};
+                    int rbs[4];
+                    uint2 q0[4], q1[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int rb = bs[k] >> 5;
+                        rbs[k] = rb < kImgRows - 1 ? rb : kImgRows - 1;
+                        q0[k] = make_uint2(w0[rbs[k]], w0[rbs[k] + 1]);
+                        q1[k] = make_uint2(w1[rbs[k]], w1[rbs[k] + 1]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int lo = 32 * rbs[k];
+                        auto ge = [&](int Y) {
+                            const int d = Y - lo;
+                            return (uint32_t)shl64_mod64(0xFFFFFFFFull, d < 0 ? 0 : (d > 32 ? 32 : d));
+                        };
+                        const uint32_t gz = ge(Z), gb = ge(B0e), ga = ge(A1), gs = ge(SP);
+                        const uint32_t x0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(q0[k].y, q0[k].x, sh0), gz, gb, 0x40);
+                        const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(q1[k].y, q1[k].x, sh1), ga, gs, 0x40);
+                        mycol[rbs[k]] =
+                            __builtin_amdgcn_bitop3_b32(x0, x1, __builtin_amdgcn_bitop3_b32(kClsDel, gb, ga, 0x40), 0xFE);
+                    }
+                }
             };
             if (!simple || (BC_ABL(A) & 16384)) {
 #pragma unroll
-                for (int row = 0; row < kImgRows; ++row) img[tid * kImgRows + row] = 0u;
+                for (int row = 0; row < kImgRows; ++row) mycol[row] = 0u;
             } else if (8 * (int64_t)(G0 + kImgRows) > A.L) {  // (uniform) rows may reach past L
                 expand(std::true_type{}, std::true_type{});
             } else {
@@ -603,10 +629,15 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const uint32_t inv = (65536u + (uint32_t)R - 1u) / (uint32_t)R;  // t / R = (t * inv) >> 16 (t < 256)
             constexpr int kPartStride = 24;                                  // >= kImgRows
             uint32_t* part = (uint32_t*)stage;                              // [q][2 NC][kPartStride]
+            // Read pairs: the words of reads r and r + 1 of the row are one ds_read2 into a register
+            // pair, and their three shifted copies (x >> 1, 2, 3) are three 64-bit shifts (the bits
+            // shifted across the halves land on nibble bits the class masks drop): 1.5 shifts per
+            // word instead of 3.
+            constexpr int kGroups = 8;
             if (tid < 8 * R && !(BC_ABL(A) & 4)) {
                 const int q = (int)(((uint32_t)tid * inv) >> 16), gr = tid - q * R;
                 uint32_t blo[6] = {0u, 0u, 0u, 0u, 0u, 0u}, bhi[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-                const uint32_t* col = img + 32 * q * kImgRows + gr;
+                const uint32_t* col = img + 32 * q * kImgRows + q * gpad + gr;
                 Swar W;
 #pragma unroll
                 for (int c = 0; c < 6; ++c) W.a4[c] = 0;
@@ -618,10 +649,29 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                         W.a4[c] = 0;
                     }
                 };
+                auto terms = [&](uint32_t x, uint32_t x1, uint32_t x2, uint32_t x3) {
+                    W.a4[0] += x & ~x1 & kM1;   // A  0001
+                    W.a4[1] += x1 & ~x & kM1;   // C  0010
+                    W.a4[2] += x2 & ~x3 & kM1;  // G  0100
+                    W.a4[3] += x3 & ~x2 & kM1;  // T  1000
+                    W.a4[4] += x2 & x3 & kM1;   // DS 1100
+                    if (NC == 6) W.a4[5] += x & x1 & kM1;  // N 0011
+                };
+                // (the 64-bit shifts are inline asm, which the scheduler does not move loads across:
+                // the words of 8 reads are loaded before any is used)
 #pragma unroll
-                for (int rr = 0; rr < 32; ++rr) {
-                    swar_add<NC>(W, col[rr * kImgRows]);
-                    if (rr == 14 || rr == 29) fold();
+                for (int r8 = 0; r8 < 32; r8 += 8) {
+                    uint32_t w[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) w[k] = col[(r8 + k) * kImgRows];
+#pragma unroll
+                    for (int k = 0; k < 8; k += 2) {
+                        const unsigned long long X = ((unsigned long long)w[k + 1] << 32) | w[k];
+                        const unsigned long long X1 = shr64<1>(X), X2 = shr64<2>(X), X3 = shr64<3>(X);
+                        terms(w[k], (uint32_t)X1, (uint32_t)X2, (uint32_t)X3);
+                        terms(w[k + 1], (uint32_t)(X1 >> 32), (uint32_t)(X2 >> 32), (uint32_t)(X3 >> 32));
+                        if (r8 + k == 12 || r8 + k == 26) fold();  // every nibble counter <= 14
+                    }
                 }
                 fold();
 #pragma unroll
@@ -633,22 +683,30 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 static_assert(8 * kImgRows <= 64 * (kRcWaves - 1), "the last wave has no image rows");
                 flush_pending(lane, 64);  // the previous image chunk's counts (8 R <= 184 < 192)
             }
+            static_assert(kGroups * 2 * 6 * kPartStride * 4 <= kStage, "the groups' partial rows fit the stage");
             __syncthreads();  // the groups' partial rows; the pending counts read
             RC_STAMP(5);
             // the rows' final counts in LDS, [class][position]
             if (tid < NC * R) {
                 const int c = (int)(((uint32_t)tid * inv) >> 16), gr = tid - c * R;
-                // byte k of the lo (hi) word = position 2k (2k + 1); 8 groups x <= 32 fits 16 bits
+                // byte k of the lo (hi) word = position 2k (2k + 1).  A group's byte is <= 32, so
+                // four groups add as bytes (<= 128); the two halves of the block then meet in
+                // 16-bit lanes (<= 256)
+                static_assert(kGroups == 8, "two halves of four 32-read groups");
                 uint32_t e = 0, o = 0, e2 = 0, o2 = 0;
                 if (!(BC_ABL(A) & 4)) {
+                    uint32_t vl[2] = {0u, 0u}, vh[2] = {0u, 0u};
 #pragma unroll
-                    for (int g8 = 0; g8 < 8; ++g8) {
-                        const uint32_t vl = part[(g8 * 2 * NC + 2 * c) * kPartStride + gr];
-                        const uint32_t vh = part[(g8 * 2 * NC + 2 * c + 1) * kPartStride + gr];
-                        e += vl & 0x00FF00FFu;         // positions 0, 4 (16-bit halves)
-                        e2 += (vl >> 8) & 0x00FF00FFu;  // positions 2, 6
-                        o += vh & 0x00FF00FFu;         // positions 1, 5
-                        o2 += (vh >> 8) & 0x00FF00FFu;  // positions 3, 7
+                    for (int g8 = 0; g8 < kGroups; ++g8) {
+                        vl[g8 >> 2] += part[(g8 * 2 * NC + 2 * c) * kPartStride + gr];
+                        vh[g8 >> 2] += part[(g8 * 2 * NC + 2 * c + 1) * kPartStride + gr];
+                    }
+#pragma unroll
+                    for (int hf = 0; hf < 2; ++hf) {
+                        e += vl[hf] & 0x00FF00FFu;         // positions 0, 4 (16-bit halves)
+                        e2 += (vl[hf] >> 8) & 0x00FF00FFu;  // positions 2, 6
+                        o += vh[hf] & 0x00FF00FFu;         // positions 1, 5
+                        o2 += (vh[hf] >> 8) & 0x00FF00FFu;  // positions 3, 7
                     }
                 }
                 uint32_t* f = fin + c * 8 * kImgRows + 8 * gr;

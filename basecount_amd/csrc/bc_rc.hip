@@ -81,6 +81,18 @@ __device__ __forceinline__ unsigned long long shr64(unsigned long long x) {
     return r;
 }
 
+// &base[i]; with a 32-bit index type as a 32-bit BYTE offset from the (uniform) base, so loads
+// and atomics address as SGPR base + 32-bit VGPR offset (no 64-bit address arithmetic per lane)
+template <typename IT, typename T>
+__device__ __forceinline__ T* elem(T* base, IT i) {
+    if constexpr (sizeof(IT) == 4) {
+        using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+        return (T*)((B*)base + (uint32_t)i * (uint32_t)sizeof(T));
+    } else {
+        return base + i;
+    }
+}
+
 struct RcArgs {
     const int32_t* pos;
     const uint32_t* cig_beg;
@@ -191,7 +203,9 @@ __device__ void rc_complex(const RcArgs& A, int64_t r, int64_t& bad) {
     }
 }
 
-template <bool QUAL, int NC, int NT>
+// IT: the type of read indices and positions (int32_t when the batch and the reference are small
+// enough, see launch_rc: uniform arithmetic then stays on the scalar unit)
+template <bool QUAL, int NC, int NT, typename IT>
 __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     using Geo = RcGeo<NT>;
     constexpr int kRcThreads = Geo::kThreads, kRcReads = Geo::kReads, kStage = Geo::kStage, kRcWaves = Geo::kWaves;
@@ -217,28 +231,29 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     uint8_t* stage = stage_raw + 4 * kPadW;
     auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     int64_t bad = INT64_MAX;
+    const IT n_reads = (IT)A.n, L = (IT)A.L, n_chunks = (IT)A.n_chunks;
 
     // run records (bc_reads.read_runs) in place of the first decode: the variants with spare
     // registers (the others spill with the extra path)
     constexpr bool kRunsOn = !QUAL && NC == 5;
     // the next chunk's per-read fields are loaded while the current one is walked
     uint32_t fpos = 0x7FFFFFFFu, fsn = 0, fcb = 0, fcn = 0, fsn_first = 0, fsn_last = 0;
-    auto fetch_fields = [&](int64_t ch) {
-        if (ch >= A.n_chunks) return;
-        const int64_t b0 = ch * kRcReads;
-        const int n = (int)(A.n - b0 < kRcReads ? A.n - b0 : kRcReads);
+    auto fetch_fields = [&](IT ch) {
+        if (ch >= n_chunks) return;
+        const IT b0 = ch * kRcReads;
+        const int n = (int)(n_reads - b0 < kRcReads ? n_reads - b0 : kRcReads);
         if (tid < n) {
-            fpos = (uint32_t)A.pos[b0 + tid];
+            fpos = (uint32_t)*elem(A.pos, b0 + tid);
             if (!kRunsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
-                fcb = A.cig_beg[b0 + tid];
-                fcn = A.cig_n[b0 + tid];
+                fcb = *elem(A.cig_beg, b0 + tid);
+                fcn = *elem(A.cig_n, b0 + tid);
             }
-            fsn = A.seq_nib[b0 + tid];
+            fsn = *elem(A.seq_nib, b0 + tid);
         }
-        fsn_first = A.seq_nib[b0];  // speculative staging bounds (reads usually lie in file order)
-        fsn_last = A.seq_nib[b0 + n - 1];
+        fsn_first = *elem(A.seq_nib, b0);  // speculative staging bounds (reads usually lie in file order)
+        fsn_last = *elem(A.seq_nib, b0 + n - 1);
     };
-    fetch_fields(blockIdx.x);
+    fetch_fields((IT)blockIdx.x);
     // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
     // with qualities and six columns, which sit at the VGPR cap without it
     constexpr bool kPfOn = !(QUAL && NC == 6);
@@ -260,22 +275,22 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     int pend_g0 = 0, pend_nw = 0;  // (uniform) the pending chunk's first window and window count
     auto flush_pending = [&](int t0, int stride) {
         for (int t = t0; t < ((BC_ABL(A) & 2048) ? 0 : 8 * pend_nw); t += stride) {
-            const int64_t p = 8 * (int64_t)pend_g0 + t;
-            if (p >= A.L) break;
+            const IT p = 8 * (IT)pend_g0 + t;
+            if (p >= L) break;
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 const uint32_t v = fin[c * 8 * kImgRows + t];
-                if (v) atomicAdd(&A.counts[(int64_t)c * A.L + p], (int32_t)v);
+                if (v) atomicAdd(elem(A.counts, (IT)c * L + p), (int32_t)v);
             }
         }
     };
 #ifdef BC_PHASE_TRACE
     uint64_t tsum[kRcPhases] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
 #endif
-    for (int64_t chunk = blockIdx.x; chunk < A.n_chunks; chunk += gridDim.x) {
+    for (IT chunk = blockIdx.x; chunk < n_chunks; chunk += (IT)gridDim.x) {
         RC_STAMP(0);
-        const int64_t c0 = chunk * kRcReads;
-        const int nr = (int)(A.n - c0 < kRcReads ? A.n - c0 : kRcReads);
+        const IT c0 = chunk * kRcReads;
+        const int nr = (int)(n_reads - c0 < kRcReads ? n_reads - c0 : kRcReads);
         // ---- 1. setup: one read per thread
         const bool valid = tid < nr;
         uint32_t mpos = 0x7FFFFFFFu, msn = 0, mcb = 0, mcn = 0;
@@ -303,8 +318,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // the CIGAR fields of a chunk read from run records: loaded only when a decode needs them
         auto cig_fields = [&]() {
             if (runs && valid) {
-                mcb = A.cig_beg[c0 + tid];
-                mcn = A.cig_n[c0 + tid];
+                mcb = *elem(A.cig_beg, c0 + tid);
+                mcn = *elem(A.cig_n, c0 + tid);
             }
         };
         // the first two runs only (all the event image needs); a chunk with more re-decodes below
@@ -329,7 +344,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             if (valid) {
                 uint4 q;
                 if (kPfOn && pf_ok) q = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-                else q = runs[c0 + tid];
+                else q = *elem(runs, c0 + tid);
                 T = unpack_runs(q.x, q.y, q.z, q.w);
             }
         } else if (BC_ABL(A) & 32768) {  // diagnostic: no CIGAR load / decode (every read one 120-base run)
@@ -361,7 +376,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         }
         uint32_t v[7];
         if (sums) {  // (uniform) reduced by the upload (bc_capi.hip chunk_summary: the same values)
-            const uint4 s0 = sums[2 * chunk], s1 = sums[2 * chunk + 1];
+            const uint4 s0 = *elem(sums, 2 * chunk), s1 = *elem(sums, 2 * chunk + 1);
             v[0] = U(s0.x), v[1] = U(s0.y), v[2] = U(s0.z), v[3] = U(s0.w);
             v[4] = U(s1.x), v[5] = U(s1.y), v[6] = U(s1.z);
             RC_STAMP(1);
@@ -381,7 +396,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
             RC_STAMP(2);
         }
-        const int64_t P0 = v[0], P1 = v[1];
+        const IT P0 = (IT)v[0], P1 = (IT)v[1];
         uint32_t seg_lo = v[2];
         const uint32_t seg_hi = v[3];
         const int maxspan = (int)v[4], maxrun = (int)v[5];
@@ -398,7 +413,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // event-image path: a staged chunk of reads with <= 2 runs whose windows fit the image.
         // Each read's events are extracted ONCE per window (lane = read, its windows in a row)
         // instead of once per (window, run) item from the run table.
-        const int64_t WBc = P0 & ~(int64_t)7;
+        const IT WBc = P0 & ~(IT)7;
         const int NWc = (int)(P1 > WBc ? (P1 - WBc + 7) / 8 : 0);
         const bool img_path = staged && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
         const int gpad = NWc;  // (uniform) the image's group padding (see rec)
@@ -455,7 +470,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
         __syncthreads();  // stage, records and the complex-read list complete
         RC_STAMP(3);
-        if (kPfOn) fetch_fields(chunk + gridDim.x);  // back before the CIGAR prefetch below
+        if (kPfOn) fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
         if (img_path) {
             // ---- event image: thread tid writes column tid, rows = the chunk's windows
             // [G0, G0 + NWc): the 8 event classes its read has in each (zero outside the read)
@@ -513,9 +528,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                         p1 = n1;
                     }
                     if (EDGE) {
-                        const int64_t rb = 8 * (int64_t)(G0 + row);  // (uniform) the row's first position
-                        if (rb + 8 > A.L) {  // events at positions >= L: the reference's out_of_range
-                            int64_t kL = A.L - rb;
+                        const IT rb = 8 * (IT)(G0 + row);  // (uniform) the row's first position
+                        if (rb + 8 > L) {  // events at positions >= L: the reference's out_of_range
+                            IT kL = L - rb;
                             kL = kL < 0 ? 0 : (kL > 8 ? 8 : kL);
                             const uint32_t bmask = ~(lo32_bit(4 * (int)kL) - 1u);
                             if ((x & bmask) && c0 + tid < bad) bad = c0 + tid;
@@ -586,7 +601,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             if (!simple || (BC_ABL(A) & 16384)) {
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) mycol[row] = 0u;
-            } else if (8 * (int64_t)(G0 + kImgRows) > A.L) {  // (uniform) rows may reach past L
+            } else if (8 * (IT)(G0 + kImgRows) > L) {  // (uniform) rows may reach past L
                 expand(std::true_type{}, std::true_type{});
             } else {
                 interior();
@@ -594,14 +609,14 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         }
         pf_ok = false;
         if (!kPfOn) {
-            fetch_fields(chunk + gridDim.x);  // in flight during the walk
-        } else if (chunk + gridDim.x < A.n_chunks) {
-            const int64_t nb0 = (chunk + gridDim.x) * kRcReads;
-            const int nn = (int)(A.n - nb0 < kRcReads ? A.n - nb0 : kRcReads);
+            fetch_fields(chunk + (IT)gridDim.x);  // in flight during the walk
+        } else if (chunk + (IT)gridDim.x < n_chunks) {
+            const IT nb0 = (chunk + (IT)gridDim.x) * kRcReads;
+            const int nn = (int)(n_reads - nb0 < kRcReads ? n_reads - nb0 : kRcReads);
             const bool nv = tid < nn;
             if (runs) {  // (uniform) the next chunk's run records instead of its CIGAR words
                 if (nv) {
-                    const uint4 q = runs[nb0 + tid];
+                    const uint4 q = *elem(runs, nb0 + tid);
                     pw[0] = q.x, pw[1] = q.y, pw[2] = q.z, pw[3] = q.w;
                 }
             } else {
@@ -613,9 +628,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         }
         const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
                          staged ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
-        const int64_t WB = P0 & ~(int64_t)7;
+        const IT WB = P0 & ~(IT)7;
         const int G0w = (int)(WB >> 3);  // the image's first window (image path)
-        const int64_t NW = P1 > WB ? (P1 - WB + 7) / 8 : 0;
+        const IT NW = P1 > WB ? (P1 - WB + 7) / 8 : 0;
         if (img_path) {
             __syncthreads();  // the image complete (columns are written by their read's thread)
             RC_STAMP(4);
@@ -925,7 +940,13 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     if (tpath && !tbuf) (void)hipMallocManaged((void**)&tbuf, tn * 8);
     if (tpath) A.trace = tbuf;
 #endif
-#define BC_RC(Q, KK) hipLaunchKernelGGL((k_rc<Q, KK, nt>), grid, block, 0, s, A)
+    // 32-bit indices when every byte offset (16 B per read, 4 B per count) fits 32 bits
+    const bool i32 = A.n < ((int64_t)1 << 27) && L < ((int64_t)1 << 27);
+#define BC_RC(Q, KK)                                                                   \
+    do {                                                                               \
+        if (i32) hipLaunchKernelGGL((k_rc<Q, KK, nt, int32_t>), grid, block, 0, s, A); \
+        else hipLaunchKernelGGL((k_rc<Q, KK, nt, int64_t>), grid, block, 0, s, A);     \
+    } while (0)
     if (mbq > 0) {
         if (ncols == 6) BC_RC(true, 6);
         else BC_RC(true, 5);

@@ -93,6 +93,13 @@ __device__ __forceinline__ T* elem(T* base, IT i) {
     }
 }
 
+// A 32-bit word at a wave-uniform address, by a scalar load (constant address space): no vector
+// memory instruction, no readfirstlane, and counted in lgkmcnt, so waiting for it does not wait for
+// the stage copy queued before it (vmcnt is in order).  Read-only data only (scalar cache).
+__device__ __forceinline__ uint32_t sload(const uint32_t* p) {
+    return *(const __attribute__((address_space(4))) uint32_t*)p;
+}
+
 struct RcArgs {
     const int32_t* pos;
     const uint32_t* cig_beg;
@@ -250,8 +257,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             }
             fsn = *elem(A.seq_nib, b0 + tid);
         }
-        fsn_first = *elem(A.seq_nib, b0);  // speculative staging bounds (reads usually lie in file order)
-        fsn_last = *elem(A.seq_nib, b0 + n - 1);
+        fsn_first = sload(elem(A.seq_nib, b0));  // speculative staging bounds (reads usually lie in file order)
+        fsn_last = sload(elem(A.seq_nib, b0 + n - 1));
     };
     fetch_fields((IT)blockIdx.x);
     // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
@@ -376,9 +383,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         }
         uint32_t v[7];
         if (sums) {  // (uniform) reduced by the upload (bc_capi.hip chunk_summary: the same values)
-            const uint4 s0 = *elem(sums, 2 * chunk), s1 = *elem(sums, 2 * chunk + 1);
-            v[0] = U(s0.x), v[1] = U(s0.y), v[2] = U(s0.z), v[3] = U(s0.w);
-            v[4] = U(s1.x), v[5] = U(s1.y), v[6] = U(s1.z);
+            const uint32_t* sw = (const uint32_t*)elem(sums, 2 * chunk);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) v[k] = sload(sw + k);
             RC_STAMP(1);
             RC_STAMP(2);
         } else {

@@ -284,11 +284,13 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         for (int t = t0; t < ((BC_ABL(A) & 2048) ? 0 : 8 * pend_nw); t += stride) {
             const IT p = 8 * (IT)pend_g0 + t;
             if (p >= L) break;
+            // the position's column counts read together (one LDS round trip), then the atomics
+            uint32_t v[NC];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const uint32_t v = fin[c * 8 * kImgRows + t];
-                if (v) atomicAdd(elem(A.counts, (IT)c * L + p), (int32_t)v);
-            }
+            for (int c = 0; c < NC; ++c) v[c] = fin[c * 8 * kImgRows + t];
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (v[c]) atomicAdd(elem(A.counts, (IT)c * L + p), (int32_t)v[c]);
         }
     };
 #ifdef BC_PHASE_TRACE

@@ -106,13 +106,16 @@ __device__ __forceinline__ uint32_t qual_nibmask(uint32_t q0, uint32_t q1, uint3
 // loads: the caller waits with stage_wait() before anything reads the stage.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
+// The pass offset is kept uniform (an SGPR: the source base, the LDS base in M0 and the loop are
+// scalar work), and only a pass that ends past `bytes` masks its lanes: a full pass costs no VALU.
 template <int NTHREADS>
 __device__ __forceinline__ void stage_dma(uint8_t* dst, const uint8_t* src, uint32_t bytes, int tid) {
-    const uint32_t wave_base = (uint32_t)(tid & ~63) * 16u;
+    const uint32_t wave_base = (uint32_t)__builtin_amdgcn_readfirstlane((tid & ~63) * 16);
+    const uint32_t l16 = (uint32_t)(tid & 63) * 16u;
     for (uint32_t off = wave_base; off < bytes; off += NTHREADS * 16u) {  // wave-uniform
-        const uint32_t mine = off + (uint32_t)(tid & 63) * 16u;
-        if (mine < bytes)
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + mine), (lds_void_t*)(dst + off), 16, 0, 0);
+        const uint8_t* s = src + off;
+        if (off + 1024u <= bytes || l16 < bytes - off)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(s + l16), (lds_void_t*)(dst + off), 16, 0, 0);
     }
 }
 __device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }

@@ -227,6 +227,7 @@ int bc_ctx_destroy(bc_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->rc_scratch) (void)hipFree(c->rc_scratch);
+    if (c->out_scratch) (void)hipFree(c->out_scratch);
     if (c->h_err) (void)hipHostFree(c->h_err);
     for (auto& v : c->ev)
         for (auto& pr : v) {
@@ -538,11 +539,66 @@ int bc_pileup(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, doub
     return BC_OK;
 }
 
+// grow-only context scratch (a synchronizing allocation when it grows: outside graph capture)
+static int out_scratch(bc_ctx* c, size_t need) {
+    if (need <= c->out_scratch_bytes) return BC_OK;
+    if (c->out_scratch) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipFree(c->out_scratch));
+        c->out_scratch = nullptr;
+        c->out_scratch_bytes = 0;
+    }
+    HIP_TRY(hipMalloc(&c->out_scratch, need));
+    c->out_scratch_bytes = need;
+    return BC_OK;
+}
+
 int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, double nf, double nf2,
                        int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent, double* d_sec, void* d_work) {
     if (!c || !r || !d_work) return fail(BC_E_ARG, "NULL argument");
     if (L <= 0) return fail(BC_E_ARG, "ref_len must be > 0 (np.mean of an empty list)");
     const bool sparse_path = !bc::use_rc(*r, L, c->shape) && r->n_reads > 0;
+    if (!d_counts && !d_cov && !d_pc && !d_ent && !d_sec) {
+        // Summary only (main.py:469-499 prints six numbers per reference): the sparse sweep writes
+        // no per-position output but the last partial buffer's coverage / entropy (into context
+        // scratch); the other paths write their outputs into context scratch.
+        if (k != 5 && k != 6) return fail(BC_E_ARG, "k must be 5 or 6");
+        DeviceGuard g(c->device);
+        if (sparse_path && L >= bc::kNpBuf) {
+            if (!r->sorted) return fail(BC_E_ARG, "bc_pileup needs a coordinate-sorted batch (sorted == 1)");
+            if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+            if (r->seq_layout != BC_SEQ_EVENT) return fail(BC_E_ARG, "bc_pileup needs seq_layout == BC_SEQ_EVENT");
+            if ((uintptr_t)r->seq & 15u) return fail(BC_E_ARG, "bc_pileup needs a 16-byte aligned sequence buffer");
+            if (int rc = out_scratch(c, (size_t)bc::kNpBuf * 12)) return rc;
+            bc::SumParts parts = bc::summary_parts(d_work, L);
+            parts.no_store = true;
+            parts.ent_tail = (double*)c->out_scratch;
+            parts.cov_tail = (int32_t*)((double*)c->out_scratch + bc::kNpBuf);
+            {
+                Timed tm(c, bc::pileup_is_solo(*r, L, c->shape, c->tile_waves) ? BC_K_SOLO : BC_K_PILEUP);
+                HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, nullptr,
+                                                nullptr, nullptr, nullptr, nullptr, c->d_err, c->shape, c->tile_waves,
+                                                &parts));
+            }
+            if (!parts.fused) return fail(BC_E_ARG, "internal: summary-only sweep without fused partials");
+            // the fold's last partial buffer reads positions [full_chunks * 8192, L): the tail
+            // arrays stand at that offset (only those elements are addressed)
+            const int64_t off = parts.full_chunks * bc::kNpBuf;
+            const int32_t* cov_base = (const int32_t*)((uintptr_t)parts.cov_tail - (uintptr_t)off * 4u);
+            const double* ent_base = (const double*)((uintptr_t)parts.ent_tail - (uintptr_t)off * 8u);
+            Timed tm(c, BC_K_SUMMARY);
+            HIP_TRY(bc::launch_summary_partials(c->stream, cov_base, ent_base, L, d_work, parts.full_chunks));
+            return BC_OK;
+        }
+        // counts [k][L] int32, cov [L] int32, ent / sec [L] double
+        const size_t need = (size_t)L * (4u * (size_t)k + 4u + 16u);
+        if (int rc = out_scratch(c, need)) return rc;
+        double* ent = (double*)c->out_scratch;
+        double* sec = ent + L;
+        int32_t* cov = (int32_t*)(sec + L);
+        int32_t* counts = cov + L;
+        return bc_pileup_partials(c, r, L, mbq, k, nf, nf2, counts, cov, nullptr, ent, sec, d_work);
+    }
     if (!sparse_path) {
         int rc = bc_pileup(c, r, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec);
         if (rc) return rc;

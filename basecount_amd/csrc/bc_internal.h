@@ -23,6 +23,8 @@ struct bc_ctx {
     hipEvent_t sig = nullptr;               // bc_ctx_wait: "everything enqueued so far"
     int32_t* rc_scratch = nullptr;         // bc_pileup's k_rc accumulation buffer, kept zeroed
     size_t rc_scratch_bytes = 0;
+    void* out_scratch = nullptr;           // bc_pileup_partials without outputs: their stand-ins
+    size_t out_scratch_bytes = 0;
     // kernel-shape overrides (bc_ctx_set_shape); 0 = chosen from the batch
     int shape = BC_SHAPE_AUTO;
     int tile_waves = 0;
@@ -73,6 +75,13 @@ struct SumParts {
     long long* sub_nz;
     bool fused;
     int64_t full_chunks;  // buffers whose partials are in the quarter arrays (fused)
+    // summary only (in): the sweep writes no per-position output except the coverage and entropy
+    // of the positions past the whole buffers, into cov_tail / ent_tail (index P - full_chunks *
+    // 8192; at most 8192 positions) for the fold's last partial buffer.  Honoured only when the
+    // sweep fuses the partials (out: fused); otherwise the caller must give full outputs.
+    bool no_store = false;
+    int32_t* cov_tail = nullptr;
+    double* ent_tail = nullptr;
 };
 // shape: BC_SHAPE_*; tile_waves: 0 = from the depth, else 1/2/4/8 waves per tile
 hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int64_t max_end, uint32_t mbq, int k,

@@ -70,6 +70,10 @@ struct PileArgs {
     long long* sub_cov;
     long long* sub_nz;
     int64_t full_chunks;
+    // k_pileup_solo without per-position stores (STORE = false, summary only): the coverage and
+    // entropy of the positions >= full_chunks * 8192 (the last partial buffer), at P - that
+    int32_t* cov_tail;
+    double* ent_tail;
     int ablate;  // diagnostic only (BC_ABLATE): 1 no reads, 2 no search, 4 no walk, 8 no stats
                  // math, 16 no stores, 32 no sequence staging
     unsigned long long* trace;  // diagnostic only (BC_TRACE): per-wave phase stamps, else null
@@ -759,8 +763,13 @@ __device__ __forceinline__ void advance_cursor(const int32_t* pos, IT n, IT& cur
 // Sparse batches: every wave owns a contiguous run of tiles and sweeps it with two read cursors
 // (no per-tile search), walks the few reads of each tile alone, and computes the statistics of
 // its own positions in registers: no block barriers at all.  Empty tiles only store.
-template <bool QUAL, int K, bool STATS, bool SUMP, typename IT>
+// STORE = false (with STATS and SUMP; bc_pileup_partials with no outputs, the summary of
+// main.py:469-499): no per-position output at all but the last partial buffer's coverage and
+// entropy; the summary partials alone are written, and a quarter buffer with no reads is one
+// constant store (its 16 leaves are 128.0 each: 2048.0, exactly).
+template <bool QUAL, int K, bool STATS, bool SUMP, typename IT, bool STORE = true>
 __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
+    static_assert(STORE || (STATS && SUMP), "the summary-only sweep computes the summary partials");
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -852,16 +861,35 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
             if (stop > t + 1) {
                 for (; t < stop; ++t) {
                     const IT tz = t * kTile;
+                    const bool whole = SUMP && (int64_t)(tz >> 13) < A.full_chunks;  // in a whole buffer
+                    if (STORE) {
 #pragma unroll
-                    for (int c = 0; c < K; ++c) (A.counts + ((int64_t)c * L + tz))[lane] = 0;
-                    (A.cov + tz)[lane] = 0;
-                    if (A.pc) {
+                        for (int c = 0; c < K; ++c) (A.counts + ((int64_t)c * L + tz))[lane] = 0;
+                        (A.cov + tz)[lane] = 0;
+                        if (A.pc) {
 #pragma unroll
-                        for (int j = 0; j < K; ++j) (A.pc + ((int64_t)j * L + tz))[lane] = -1.0;
+                            for (int j = 0; j < K; ++j) (A.pc + ((int64_t)j * L + tz))[lane] = -1.0;
+                        }
+                        (A.ent + tz)[lane] = 1.0;
+                        (A.sec + tz)[lane] = 1.0;
+                    } else if (!whole) {  // the last partial buffer: coverage 0, entropy 1
+                        const int64_t i = (int64_t)tz - A.full_chunks * kNpBuf + lane;
+                        A.cov_tail[i] = 0;
+                        A.ent_tail[i] = 1.0;
+                        continue;
+                    } else if ((t & 31) == 0 && t + 32 <= stop) {
+                        // a whole quarter without reads (32 tiles, one subtree of numpy's tree;
+                        // the quarters before it left the coverage sums at 0)
+                        if (lane == 0) {
+                            const int64_t q = (int64_t)(t >> 5);
+                            A.sub_ent[q] = 2048.0;
+                            A.sub_cov[q] = 0;
+                            A.sub_nz[q] = 0;
+                        }
+                        t += 31;
+                        continue;
                     }
-                    (A.ent + tz)[lane] = 1.0;
-                    (A.sec + tz)[lane] = 1.0;
-                    if (SUMP && (int64_t)(tz >> 13) < A.full_chunks) leaf_step(t, true, 1.0);
+                    if (whole) leaf_step(t, true, 1.0);
                 }
                 --t;  // the loop's increment moves to `stop`
                 continue;
@@ -902,7 +930,21 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
             }
         }
         const bool empty = hi <= lo;  // (uniform) no read overlaps the tile: all counts zero
-        if (t0 < L && P < L && !(BC_ABL(A) & 16)) {
+        if (!STORE && t0 < L && P < L) {  // summary only: coverage and entropy, no stores
+            uint32_t cov;
+            const double h = position_entropy<K>(cnt, A.nf, cov);
+            if ((int64_t)(t0 >> 13) < A.full_chunks) {
+                if (!empty) {
+                    sum_cov += cov;
+                    sum_nz += cov != 0;
+                }
+                leaf_step(t, empty, h);
+            } else {
+                const int64_t i = (int64_t)P - A.full_chunks * kNpBuf;
+                A.cov_tail[i] = (int32_t)cov;
+                A.ent_tail[i] = h;
+            }
+        } else if (STORE && t0 < L && P < L && !(BC_ABL(A) & 16)) {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
                 int32_t* cb = A.counts + ((int64_t)c * L + t0);  // (uniform)
@@ -996,6 +1038,7 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         A.tiles_per_wave = (A.n_tiles + target_waves - 1) / target_waves;
         if (A.tiles_per_wave < 1) A.tiles_per_wave = 1;
         const bool sump = parts && stats && L >= kNpBuf;
+        const bool nostore = sump && parts->no_store;
         if (sump) {  // whole quarter buffers per wave: the summary partials come for free
             A.tiles_per_wave = (A.tiles_per_wave + 31) / 32 * 32;
             A.sub_ent = parts->sub_ent;
@@ -1004,6 +1047,8 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
             A.full_chunks = L / kNpBuf;
             parts->fused = true;
             parts->full_chunks = A.full_chunks;
+            A.cov_tail = parts->cov_tail;
+            A.ent_tail = parts->ent_tail;
         }
         const int64_t waves = (A.n_tiles + A.tiles_per_wave - 1) / A.tiles_per_wave;
         int64_t blocks = (waves + nw - 1) / nw;
@@ -1014,7 +1059,10 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         const bool i32 = A.n < (int64_t)0x7FFFFF00 && A.n_tiles * kTile + A.max_span + 2 * kTile < (int64_t)0x7FFFFF00;
 #define BC_SOLO(Q, KK, ST)                                                                                       \
     do {                                                                                                         \
-        if (sump && i32) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true, int32_t>), grid, block, lds, s, A); \
+        if (nostore && i32)                                                                                      \
+            hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true, int32_t, false>), grid, block, lds, s, A);      \
+        else if (nostore) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true, int64_t, false>), grid, block, lds, s, A); \
+        else if (sump && i32) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true, int32_t>), grid, block, lds, s, A); \
         else if (sump) hipLaunchKernelGGL((k_pileup_solo<Q, KK, true, true, int64_t>), grid, block, lds, s, A);   \
         else if (i32) hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST, false, int32_t>), grid, block, lds, s, A);     \
         else hipLaunchKernelGGL((k_pileup_solo<Q, KK, ST, false, int64_t>), grid, block, lds, s, A);              \

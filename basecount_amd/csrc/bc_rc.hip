@@ -47,6 +47,29 @@ constexpr uint32_t kSpecSlack = 128;  // bytes staged beyond the last read's fir
 #include "bc_walk.h"
 static_assert(kRcChunk == kRcChunkReads, "the upload summarises chunks of k_rc's size (bc_runs.h)");
 
+// the image's CIGAR decode by decode_fast2 (bc_runs.h); -DBC_FAST_DECODE=0 builds the A/B variant
+// that decodes every chunk with decode_runs
+#ifndef BC_FAST_DECODE
+#define BC_FAST_DECODE 1
+#endif
+constexpr bool kFastDecode = BC_FAST_DECODE != 0;
+// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding: vmcnt [3:0] and
+// [15:14], expcnt [6:4], lgkmcnt [11:8]); as a builtin the compiler's waitcnt pass sees it
+constexpr int kWaitVm0 = 0x0F70;
+#ifndef BC_RC_EARLY_WAIT
+#define BC_RC_EARLY_WAIT 1
+#endif
+constexpr bool kEarlyWait = BC_RC_EARLY_WAIT != 0;
+// chunk bounds without the index: reduced across the waves at the stage barrier (see `deferred`);
+// -DBC_RC_DEFER_BOUNDS=0 builds the A/B variant with its own block reduction barrier
+#ifndef BC_RC_DEFER_BOUNDS
+#define BC_RC_DEFER_BOUNDS 1
+#endif
+constexpr bool kDeferBounds = BC_RC_DEFER_BOUNDS != 0;
+#ifndef BC_RC_IGNORE_RECORDS
+#define BC_RC_IGNORE_RECORDS 0
+#endif
+
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
 constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
 
@@ -79,6 +102,55 @@ __device__ __forceinline__ unsigned long long shr64(unsigned long long x) {
     unsigned long long r;
     asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
     return r;
+}
+
+// ---- bit-sliced counting (the event image's transposed sum) ----------------------------------
+// A full adder over 32 bit positions at once: s = a ^ b ^ c, k = maj(a, b, c) (one v_bitop3 each)
+__device__ __forceinline__ void fadd(uint32_t& s, uint32_t& k, uint32_t a, uint32_t b, uint32_t c) {
+    s = __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+    k = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+// Harley-Seal carry-save tree over 16 words: adds their bits into the bit-sliced digits d[0..3]
+// (weights 1, 2, 4, 8) and returns the carry word of weight 16 (15 full adders, 30 VALU).
+__device__ __forceinline__ uint32_t csa16(uint32_t* d, const uint32_t* x) {
+    uint32_t tA, tB, fA, fB, eA, eB, s16;
+    fadd(d[0], tA, d[0], x[0], x[1]);
+    fadd(d[0], tB, d[0], x[2], x[3]);
+    fadd(d[1], fA, d[1], tA, tB);
+    fadd(d[0], tA, d[0], x[4], x[5]);
+    fadd(d[0], tB, d[0], x[6], x[7]);
+    fadd(d[1], fB, d[1], tA, tB);
+    fadd(d[2], eA, d[2], fA, fB);
+    fadd(d[0], tA, d[0], x[8], x[9]);
+    fadd(d[0], tB, d[0], x[10], x[11]);
+    fadd(d[1], fA, d[1], tA, tB);
+    fadd(d[0], tA, d[0], x[12], x[13]);
+    fadd(d[0], tB, d[0], x[14], x[15]);
+    fadd(d[1], fB, d[1], tA, tB);
+    fadd(d[2], eB, d[2], fA, fB);
+    fadd(d[3], s16, d[3], eA, eB);
+    return s16;
+}
+// In-register transpose of 8 x (4 blocks of 8 x 8 bits): afterwards byte i of r[k] holds, in bit d,
+// bit 8i + k of the input r[d] (three rounds of block swaps, two v_bfi_b32 and two shifts each).
+// With bit-sliced digits r[d] this turns the 32 bit positions' counts into bytes.
+__device__ __forceinline__ void bit_transpose8(uint32_t (&r)[8]) {
+    auto swap = [&](int a, int b, int s, uint32_t m) {  // r[a] bits (k + s) <-> r[b] bits k, k in m
+        const uint32_t ra = r[a], rb = r[b];
+        // bitop3 0xCA = bit select (m ? x : y), kept as written (the compiler's own form of the
+        // selects took ~2x the instructions)
+        r[b] = __builtin_amdgcn_bitop3_b32(m, ra >> s, rb, 0xCA);
+        r[a] = __builtin_amdgcn_bitop3_b32(m << s, rb << s, ra, 0xCA);
+    };
+#pragma unroll
+    for (int d = 0; d < 4; ++d) swap(d, d + 4, 4, 0x0F0F0F0Fu);
+#pragma unroll
+    for (int d = 0; d < 8; d += 4) {
+        swap(d, d + 2, 2, 0x33333333u);
+        swap(d + 1, d + 3, 2, 0x33333333u);
+    }
+#pragma unroll
+    for (int d = 0; d < 8; d += 2) swap(d, d + 1, 1, 0x55555555u);
 }
 
 // &base[i]; with a 32-bit index type as a 32-bit BYTE offset from the (uniform) base, so loads
@@ -127,8 +199,11 @@ struct RcArgs {
 // Block-wide reduction of NV <= 8 values (max or min per slot): wave reduce, then LDS across
 // waves.  Lane k of each wave stores slot k (one masked store, not one per slot); every thread
 // then reads the waves' rows as 16-byte words.  Must be called by the whole block.
-template <int NV, int NWAVES>
-__device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
+// wave_partials (each wave's results into its row of red) + a barrier + block_combine (every thread
+// folds the rows); k_rc calls the two halves around its stage barrier when it can (no extra
+// barrier in the chunk chain).
+template <int NV>
+__device__ __forceinline__ void wave_partials(const uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
     static_assert(NV <= 8, "one 8-word row per wave");
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t mine = 0;
@@ -138,7 +213,9 @@ __device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_
         mine = lane == k ? r : mine;
     }
     if (lane < NV) red[wave][lane] = mine;
-    __syncthreads();
+}
+template <int NV, int NWAVES>
+__device__ __forceinline__ void block_combine(uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
     uint32_t w[NWAVES][8];
 #pragma unroll
     for (int q = 0; q < NWAVES; ++q) {
@@ -153,6 +230,12 @@ __device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_
         for (int q = 1; q < NWAVES; ++q) r = is_max[k] ? (w[q][k] > r ? w[q][k] : r) : (w[q][k] < r ? w[q][k] : r);
         v[k] = r;
     }
+}
+template <int NV, int NWAVES>
+__device__ __forceinline__ void block_reduce(uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
+    wave_partials<NV>(v, is_max, red);
+    __syncthreads();
+    block_combine<NV, NWAVES>(v, is_max, red);
 }
 
 // Fold a wave's window counters into the LDS histogram: 8-slot sums per lane group (DPP), then
@@ -243,6 +326,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // run records (bc_reads.read_runs) in place of the first decode: the variants with spare
     // registers (the others spill with the extra path)
     constexpr bool kRunsOn = !QUAL && NC == 5;
+    // A/B only (-DBC_RC_IGNORE_RECORDS=1): decode the CIGARs but take the chunk summaries
+    constexpr bool kRecordsOn = kRunsOn && !BC_RC_IGNORE_RECORDS;
     // the next chunk's per-read fields are loaded while the current one is walked
     uint32_t fpos = 0x7FFFFFFFu, fsn = 0, fcb = 0, fcn = 0, fsn_first = 0, fsn_last = 0;
     auto fetch_fields = [&](IT ch) {
@@ -251,7 +336,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const int n = (int)(n_reads - b0 < kRcReads ? n_reads - b0 : kRcReads);
         if (tid < n) {
             fpos = (uint32_t)*elem(A.pos, b0 + tid);
-            if (!kRunsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
+            if (!kRecordsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
                 fcb = *elem(A.cig_beg, b0 + tid);
                 fcn = *elem(A.cig_n, b0 + tid);
             }
@@ -264,7 +349,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
     // with qualities and six columns, which sit at the VGPR cap without it
     constexpr bool kPfOn = !(QUAL && NC == 6);
-    const uint4* const runs = kRunsOn ? A.runs : nullptr;
+    const uint4* const runs = kRecordsOn ? A.runs : nullptr;
     // the upload's chunk summaries: the chunk bounds without the block reduction (and its barrier)
     const uint4* const sums = kRunsOn && A.runs ? A.sums : nullptr;
     if (tid < 2) ncx[tid] = 0;
@@ -317,6 +402,12 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const uint32_t buf_end = (uint32_t)(A.seq_words * 4 < 0xFFFFFFFFll ? A.seq_words * 4 : 0xFFFFFFFFll);
         spec_hi = spec_hi < buf_end ? spec_hi : buf_end;
         const bool spec = !QUAL && spec_hi > spec_lo && spec_hi - spec_lo <= (uint32_t)kStage && !(BC_ABL(A) & 512);
+        // The loads prefetched during the previous chunk (fields, run records or CIGAR words) are
+        // waited for HERE, before the stage DMA is queued behind them: vmcnt is in order and the
+        // compiler cannot count the DMA passes, so a wait at their first use below would be a
+        // vmcnt(0) that also waits for this chunk's whole stage copy (the decode then sat behind
+        // the copy's round trip).  They were issued a whole phase ago: this wait is ~free.
+        if (kEarlyWait) __builtin_amdgcn_s_waitcnt(kWaitVm0);
         if (spec) stage_dma<kRcThreads>(stage, A.seq + spec_lo, spec_hi - spec_lo, tid);
         RunTable T;
         T.nrun = 0;
@@ -337,23 +428,33 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             if (valid) {
                 uint32_t w[kPre];
                 const bool use_pf = kPfOn && pf_ok && !runs && cmax <= kPf;  // (uniform)
+                if (use_pf) {
 #pragma unroll
-                for (int i = 0; i < kPre; ++i) {
-                    w[i] = 0u;
-                    if (use_pf && i < kPf) {
-                        w[i] = pw[i];
-                        continue;
-                    }
-                    if (!use_pf && i < cmax && (uint32_t)i < mcn) w[i] = A.cigar[mcb + i];
+                    for (int i = 0; i < kPre; ++i) w[i] = i < kPf ? pw[i] : 0u;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < kPre; ++i) w[i] = (i < cmax && (uint32_t)i < mcn) ? A.cigar[mcb + i] : 0u;
+                    // waited for on this path only: the prefetched words need no wait (kEarlyWait)
+                    if (kEarlyWait) __builtin_amdgcn_s_waitcnt(kWaitVm0);
                 }
-                T = decode_runs<decltype(nslot)::value>(w, mcn, cmax);
+                if constexpr (decltype(nslot)::value == 2 && kFastDecode) {
+                    // the lane's scratch: the image region, dead until this chunk's barrier below
+                    const bool ok = decode_fast2(w, mcn, cmax, img + 8 * tid, T);
+                    if (__ballot(!ok)) T = decode_runs<2>(w, mcn, cmax);  // (uniform) a read with > 2 runs
+                } else {
+                    T = decode_runs<decltype(nslot)::value>(w, mcn, cmax);
+                }
             }
         };
         if (runs) {  // (uniform) the upload's run records: no CIGAR load, no decode
             if (valid) {
                 uint4 q;
-                if (kPfOn && pf_ok) q = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-                else q = *elem(runs, c0 + tid);
+                if (kPfOn && pf_ok) {
+                    q = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+                } else {
+                    q = *elem(runs, c0 + tid);
+                    if (kEarlyWait) __builtin_amdgcn_s_waitcnt(kWaitVm0);  // (this path only, as above)
+                }
                 T = unpack_runs(q.x, q.y, q.z, q.w);
             }
         } else if (BC_ABL(A) & 32768) {  // diagnostic: no CIGAR load / decode (every read one 120-base run)
@@ -384,6 +485,13 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             cspan = sp > 0x3FFFFFFFu ? 0x3FFFFFFFu : (uint32_t)sp;
         }
         uint32_t v[7];
+        const bool is_max[7] = {false, true, false, true, true, true, true};
+        // (uniform) without the index's summaries and qualities: each wave reduces its share of the
+        // chunk bounds now and the block combines them after the stage barrier, assuming the
+        // speculative stage and the event image (a chunk for which either is wrong restages /
+        // writes run tables after that barrier and meets at a second one): the chunk chain has no
+        // barrier more than with the summaries
+        const bool deferred = !sums && !QUAL && kDeferBounds;
         if (sums) {  // (uniform) reduced by the upload (bc_capi.hip chunk_summary: the same values)
             const uint32_t* sw = (const uint32_t*)elem(sums, 2 * chunk);
 #pragma unroll
@@ -400,9 +508,16 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             // at its end) count as 3 runs: such a chunk takes the run tables
             v[5] = simple ? run_shape(T) : 0u;
             v[6] = (simple && T.gap) ? 1u : 0u;
-            const bool is_max[7] = {false, true, false, true, true, true, true};
             RC_STAMP(1);
-            block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
+            if (deferred) {
+                wave_partials<7>(v, is_max, red);
+                if (cx) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
+                stage_wait();     // this thread's speculative LDS-DMA landed
+                __syncthreads();  // the stage, the complex-read list and the waves' partial bounds
+                block_combine<7, kRcWaves>(v, is_max, red);
+            } else {
+                block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
+            }
             RC_STAMP(2);
         }
         const IT P0 = (IT)v[0], P1 = (IT)v[1];
@@ -415,7 +530,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             decode(std::integral_constant<int, kMaxRuns>{});
         }
         seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
-        if (cx) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
+        if (cx && !deferred) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
         if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
         const bool staged = spec_ok || seg_hi - seg_lo <= (uint32_t)kStage;
@@ -427,7 +542,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const bool img_path = staged && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
         const int gpad = NWc;  // (uniform) the image's group padding (see rec)
         uint32_t* const mycol = img + tid * kImgRows + (tid >> 5) * gpad;  // this read's image column
-        if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
+        if (spec && !spec_ok && !deferred) {  // (uniform) the speculative copy is overwritten
             stage_wait();
             __syncthreads();
         }
@@ -476,8 +591,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             }
             if (!img_path) rpos[tid] = (int32_t)mpos;  // (the window tables of the run-table walk)
         }
-        if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
-        __syncthreads();  // stage, records and the complex-read list complete
+        if (!deferred || !spec_ok || !img_path) {  // (uniform) deferred: only a chunk that restaged or wrote records
+            if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
+            __syncthreads();  // stage, records and the complex-read list complete
+        }
         RC_STAMP(3);
         if (kPfOn) fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
         if (img_path) {
@@ -660,44 +777,50 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             constexpr int kGroups = 8;
             if (tid < 8 * R && !(BC_ABL(A) & 4)) {
                 const int q = (int)(((uint32_t)tid * inv) >> 16), gr = tid - q * R;
-                uint32_t blo[6] = {0u, 0u, 0u, 0u, 0u, 0u}, bhi[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+                uint32_t blo[6], bhi[6];
                 const uint32_t* col = img + 32 * q * kImgRows + q * gpad + gr;
-                Swar W;
+                // Bit-sliced: a row word's 32 bits are (position j, plane p) = bit 4j + p of the
+                // class nibble.  A carry-save tree counts every bit position over the 32 reads at
+                // once (digits xd: plane counts A+N, C+N, G+DS, T+DS); the N (0011) and DS (1100)
+                // planes, b0 & b1 and b2 & b3 of a nibble, are counted the same way with two reads
+                // packed per word (yd).  A bit transpose turns the digits into byte counters.
+                uint32_t xd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, yd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+                uint32_t y[16], x16 = 0u;
 #pragma unroll
-                for (int c = 0; c < 6; ++c) W.a4[c] = 0;
-                auto fold = [&]() {
+                for (int h = 0; h < 2; ++h) {
+                    uint32_t w[16];
 #pragma unroll
-                    for (int c = 0; c < NC; ++c) {
-                        blo[c] += W.a4[c] & 0x0F0F0F0Fu;
-                        bhi[c] += (W.a4[c] >> 4) & 0x0F0F0F0Fu;
-                        W.a4[c] = 0;
+                    for (int k = 0; k < 16; ++k) w[k] = col[(16 * h + k) * kImgRows];
+#pragma unroll
+                    for (int k = 0; k < 16; k += 2) {
+                        const unsigned long long X1 = shr64<1>(((unsigned long long)w[k + 1] << 32) | w[k]);
+                        // bits 4j / 4j + 2: N / DS of read k; 4j + 1 / 4j + 3: those of read k + 1
+                        const uint32_t ya = __builtin_amdgcn_bitop3_b32(w[k], (uint32_t)X1, 0x55555555u, 0x80);
+                        const uint32_t yb = __builtin_amdgcn_bitop3_b32(w[k + 1], (uint32_t)(X1 >> 32), 0x55555555u, 0x80);
+                        y[8 * h + k / 2] = (yb << 1) | ya;
                     }
-                };
-                auto terms = [&](uint32_t x, uint32_t x1, uint32_t x2, uint32_t x3) {
-                    W.a4[0] += x & ~x1 & kM1;   // A  0001
-                    W.a4[1] += x1 & ~x & kM1;   // C  0010
-                    W.a4[2] += x2 & ~x3 & kM1;  // G  0100
-                    W.a4[3] += x3 & ~x2 & kM1;  // T  1000
-                    W.a4[4] += x2 & x3 & kM1;   // DS 1100
-                    if (NC == 6) W.a4[5] += x & x1 & kM1;  // N 0011
-                };
-                // (the 64-bit shifts are inline asm, which the scheduler does not move loads across:
-                // the words of 8 reads are loaded before any is used)
-#pragma unroll
-                for (int r8 = 0; r8 < 32; r8 += 8) {
-                    uint32_t w[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) w[k] = col[(r8 + k) * kImgRows];
-#pragma unroll
-                    for (int k = 0; k < 8; k += 2) {
-                        const unsigned long long X = ((unsigned long long)w[k + 1] << 32) | w[k];
-                        const unsigned long long X1 = shr64<1>(X), X2 = shr64<2>(X), X3 = shr64<3>(X);
-                        terms(w[k], (uint32_t)X1, (uint32_t)X2, (uint32_t)X3);
-                        terms(w[k + 1], (uint32_t)(X1 >> 32), (uint32_t)(X2 >> 32), (uint32_t)(X3 >> 32));
-                        if (r8 + k == 12 || r8 + k == 26) fold();  // every nibble counter <= 14
+                    const uint32_t c16 = csa16(xd, w);
+                    if (h == 0) {
+                        x16 = c16;
+                    } else {
+                        xd[4] = x16 ^ c16;
+                        xd[5] = x16 & c16;
                     }
                 }
-                fold();
+                yd[4] = csa16(yd, y);
+                bit_transpose8(xd);  // xd[4h + p]: plane p, byte i = position 2i + h (<= 32)
+                bit_transpose8(yd);  // yd[4h + 0/1]: N of even / odd reads, 4h + 2/3: DS (<= 16)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t nn = yd[4 * h] + yd[4 * h + 1], ds = yd[4 * h + 2] + yd[4 * h + 3];
+                    uint32_t* o = h ? bhi : blo;
+                    o[0] = xd[4 * h] - nn;  // bytes: no borrow (plane count >= its N / DS count)
+                    o[1] = xd[4 * h + 1] - nn;
+                    o[2] = xd[4 * h + 2] - ds;
+                    o[3] = xd[4 * h + 3] - ds;
+                    o[4] = ds;
+                    o[5] = nn;
+                }
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     part[(q * 2 * NC + 2 * c) * kPartStride + gr] = blo[c];

@@ -114,6 +114,74 @@ BC_HD RunTable unpack_runs(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     return T;
 }
 
+// ---- the CIGAR decode of the event image (the first two runs), ~12 VALU per op ------------------
+// decode_runs updates a whole run table through selects at every op (~33 VALU per op).  Here each
+// op only adds its reference / query lengths into a packed prefix P[k] = rc | qc << 16 (before op
+// k) and marks itself in a bit string F (bit 2k: M/=/X, bit 2k + 1: I/D/N, zero lengths
+// excluded).  Runs are the M groups between I/D/N ops, so the op indices where they start and end
+// are found bit-parallel (v_ffbl on F), and their bounds are P at those indices (one LDS round
+// trip through the lane's own 8 scratch words, `scr`, 16-byte aligned).  The result equals decode_runs<2>'s table
+// whenever the read has at most two runs and every op length is below 2^13; the function returns
+// false otherwise (the caller then runs decode_runs).
+BC_HD uint32_t ffbl_or_none(uint32_t x) { return (uint32_t)(__builtin_ffs((int)x) - 1); }  // 0xFFFFFFFF if x == 0
+// bits [off & 31, (off & 31) + w) of x (one v_bfe_u32 on the device)
+BC_HD uint32_t ubfe(uint32_t x, uint32_t off, uint32_t w) { return (x >> (off & 31u)) & ((1u << w) - 1u); }
+BC_HD bool decode_fast2(const uint32_t (&w)[kPre], uint32_t cn, int cmax, uint32_t* scr,
+                     RunTable& T) {
+    // 2-bit fields at 2 * op: kMB 1 = M/=/X (0, 7, 8), 2 = I/D/N (1, 2, 3); kRQ bit 0 = consumes the
+    // reference (M D N = X), bit 1 = consumes the query (M I = X)
+    constexpr uint32_t kMB = 1u | 2u << 2 | 2u << 4 | 2u << 6 | 1u << 14 | 1u << 16;
+    constexpr uint32_t kRQ = 3u | 2u << 2 | 1u << 4 | 1u << 6 | 3u << 14 | 3u << 16;
+    uint32_t P[kPre + 1];
+    P[0] = 0u;
+    uint32_t F = 0u, big = 0u;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+        if (k >= cmax) {  // (uniform) no lane has more ops
+            P[k + 1] = P[k];
+            continue;
+        }
+        const uint32_t o2 = w[k] << 1, len = w[k] >> 4;  // v_bfe reads the low 5 bits of o2: 2 * op
+        uint32_t fl = ubfe(kMB, o2, 2);
+        fl = fl < (len << 1) ? fl : (len << 1);  // zero-length ops are no run and no break
+        F |= fl << (2 * k);
+        const uint32_t rq = ubfe(kRQ, o2, 2);
+        P[k + 1] = P[k] + (len & 0xFFFFFFu) * ((rq * 0x8001u) & 0x10001u);  // rq -> 1 | 1 << 16 (v_mad_u32_u24)
+        big |= len;
+    }
+    uint32_t* s16 = (uint32_t*)__builtin_assume_aligned(scr, 16);
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) s16[k] = P[k];
+    scr = s16;
+    const uint32_t Mb = F & 0x5555u, Bb = (F >> 1) & 0x5555u;
+    // first M op, the first I/D/N after it, the next M (run 1), the next I/D/N, a third run
+    const uint32_t p1 = ffbl_or_none(Mb);
+    const uint32_t p2 = ffbl_or_none(Bb & (0xFFFFFFFFu << (p1 & 31u)));
+    const uint32_t p3 = ffbl_or_none(Mb & (0xFFFFFFFFu << (p2 & 31u)));
+    const uint32_t p4 = ffbl_or_none(Bb & (0xFFFFFFFFu << (p3 & 31u)));
+    const uint32_t p5 = ffbl_or_none(Mb & (0xFFFFFFFFu << (p4 & 31u)));
+    const uint32_t X1 = scr[(p1 >> 1) & 7u], X2 = scr[(p2 >> 1) & 7u], X3 = scr[(p3 >> 1) & 7u],
+                   X4 = scr[(p4 >> 1) & 7u];
+    const uint32_t span = P[kPre] & 0xFFFFu;
+    const int nrun = p1 == 0xFFFFFFFFu ? 0 : (p3 == 0xFFFFFFFFu ? 1 : (p5 == 0xFFFFFFFFu ? 2 : 3));
+    T.span = span;
+    T.qlen = P[kPre] >> 16;
+    T.nrun = nrun;
+    T.st[2] = T.en[2] = T.st[3] = T.en[3] = 0u;
+    T.qd[2] = T.qd[3] = 0;
+    T.st[0] = nrun >= 1 ? X1 & 0xFFFFu : 0u;
+    T.qd[0] = nrun >= 1 ? (int)(X1 >> 16) - (int)(X1 & 0xFFFFu) : 0;
+    T.en[0] = nrun >= 1 ? (p2 != 0xFFFFFFFFu ? X2 & 0xFFFFu : span) : 0u;
+    T.st[1] = nrun >= 2 ? X3 & 0xFFFFu : 0u;
+    T.qd[1] = nrun >= 2 ? (int)(X3 >> 16) - (int)(X3 & 0xFFFFu) : 0;
+    T.en[1] = nrun >= 2 ? (p4 != 0xFFFFFFFFu ? X4 & 0xFFFFu : span) : 0u;
+    // a deletion / ref-skip of positive length <=> the span exceeds the runs' lengths
+    T.gap = span != (T.en[0] - T.st[0]) + (T.en[1] - T.st[1]);
+    const bool qd_ok = T.qd[0] >= -32768 && T.qd[0] <= 32767 && T.qd[1] >= -32768 && T.qd[1] <= 32767;
+    T.complex = cn > (uint32_t)kPre || !qd_ok || span >= 0x1FFFu;
+    return cn > (uint32_t)kPre || (nrun <= 2 && big < 0x2000u);
+}
+
 // ---- chunk summaries of the read-chunked kernel (bc_reads.read_runs after the records) ----
 constexpr int kRcChunkReads = 256;  // reads per k_rc chunk (one per thread of its block)
 

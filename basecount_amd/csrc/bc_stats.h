@@ -59,4 +59,26 @@ __device__ __forceinline__ double position_stats(const uint32_t* c, int64_t L, i
     return h;
 }
 
+// The coverage and the entropy of position_stats alone (the same operations in the same order,
+// so the same bits), for the summary-only sweep: main.py:469-499 averages coverage and entropy
+// only, and neither the percentages nor the secondary entropy are computed.
+template <int K>
+__device__ __forceinline__ double position_entropy(const uint32_t* c, double nf, uint32_t& cov_out) {
+    int64_t cov = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) cov += c[j];
+    cov_out = (uint32_t)cov;
+    double h = 1.0;
+    if (cov != 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const double pj = (double)c[j] / (double)cov;
+            if (c[j] != 0) s = s + (-(pj * glibc_log2(pj)));
+        }
+        h = nf * s;
+    }
+    return h;
+}
+
 }  // namespace bc

@@ -26,6 +26,7 @@ rank reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import json
 import os
@@ -105,49 +106,146 @@ def _rdzv_timeout() -> float:
     return float(v) if v else 120.0
 
 
-def rendezvous_id(rank: int, world: int, make_id, timeout: float | None = None) -> bytes:
-    """Rank 0 calls make_id() and sends the bytes to every other rank over TCP (port
-    ``BASECOUNT_RDZV_PORT``, default MASTER_PORT + 1).  The other ranks retry the connection
-    for ``timeout`` seconds (``BASECOUNT_RDZV_TIMEOUT``, default 120); rank 0 fails at once,
-    with the port in the message, if the port is taken."""
+class CommInitError(RuntimeError):
+    """The job's communicator could not be created on every rank.  Raised on EVERY rank (the ranks
+    vote, see rendezvous_init), so a caller that falls back (bench.py: gloo) does so on all ranks
+    alike and no rank is left waiting in a collective the others never join."""
+
+
+def _init_timeout() -> float:
+    v = os.environ.get("BASECOUNT_COMM_INIT_TIMEOUT")
+    return float(v) if v else 120.0
+
+
+def _run_with_timeout(fn, arg, timeout: float):
+    """fn(arg) in a daemon thread: (True, result) or (False, reason).  A call still blocked at the
+    timeout (a collective init whose peers never arrive) is abandoned with its thread."""
+    import threading
+
+    box = {}
+
+    def target():
+        try:
+            box["v"] = (True, fn(arg))
+        except Exception as e:  # noqa: BLE001 - reported to the other ranks, re-raised by the caller
+            box["v"] = (False, f"{type(e).__name__}: {e}")
+
+    t = threading.Thread(target=target, daemon=True)
+    t.start()
+    t.join(timeout)
+    return box.get("v", (False, f"no result within {timeout:.0f} s (BASECOUNT_COMM_INIT_TIMEOUT)"))
+
+
+def rendezvous_init(rank: int, world: int, make_id, init, timeout: float | None = None,
+                    init_timeout: float | None = None):
+    """A communicator created by agreement of all ranks, over one TCP connection per peer to rank
+    0 (port ``BASECOUNT_RDZV_PORT``, default MASTER_PORT + 1):
+
+      1. rank 0 binds the port (failing at once, with the port in the message, if it is taken),
+         calls make_id() and sends its bytes to every peer (an empty id if make_id failed: every
+         rank then raises at once instead of waiting);
+      2. every rank calls init(id) (the collective bc_comm_init) in a thread bounded by
+         ``init_timeout`` (``BASECOUNT_COMM_INIT_TIMEOUT``, default 120 s);
+      3. every rank reports success or failure to rank 0, which answers all of them with the
+         verdict.  Unless every rank succeeded, every rank raises CommInitError, naming the
+         ranks that failed.
+
+    The peers retry the connection for ``timeout`` seconds (``BASECOUNT_RDZV_TIMEOUT``, default
+    120).  Returns init's result."""
     addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = _rdzv_port()
     timeout = _rdzv_timeout() if timeout is None else float(timeout)
+    init_timeout = _init_timeout() if init_timeout is None else float(init_timeout)
     deadline = time.monotonic() + timeout
+
+    def verdict_of(statuses: list):
+        bad = [f"rank {r}: {w}" for r, (o, w) in enumerate(statuses) if not o]
+        return not bad, "; ".join(bad)
+
     if rank == 0:
-        uid = make_id()
-        if world == 1:
-            return uid
-        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        srv = None
+        if world > 1:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            try:
+                srv.bind((addr, port))
+            except OSError as e:
+                srv.close()
+                raise RuntimeError(f"rank 0 cannot bind the rendezvous port {addr}:{port} ({e}); set "
+                                   "BASECOUNT_RDZV_PORT to a free port") from e
+            srv.listen(max(1, world))
+            srv.settimeout(timeout)
+        conns = []
         try:
-            srv.bind((addr, port))
-        except OSError as e:
-            srv.close()
-            raise RuntimeError(f"rank 0 cannot bind the rendezvous port {addr}:{port} ({e}); set "
-                               "BASECOUNT_RDZV_PORT to a free port") from e
-        srv.listen(max(1, world))
-        srv.settimeout(timeout)
-        try:
-            for _ in range(world - 1):
-                conn, _ = srv.accept()
-                with conn:
-                    _recv_exact(conn, 4)  # the peer's rank (kept for debugging)
-                    conn.sendall(struct.pack("<I", len(uid)) + uid)
+            try:
+                uid, id_err = make_id(), None
+            except Exception as e:  # noqa: BLE001 - every peer is told, then it is re-raised
+                uid, id_err = b"", e
+            while srv is not None and len(conns) < world - 1:
+                try:
+                    conn, _ = srv.accept()
+                except socket.timeout as e:
+                    raise CommInitError(f"rank 0: only {len(conns)} of {world - 1} peers reached the "
+                                        f"rendezvous at {addr}:{port} within {timeout:.0f} s") from e
+                conn.settimeout(init_timeout + timeout)
+                peer = struct.unpack("<I", _recv_exact(conn, 4))[0]
+                conn.sendall(struct.pack("<I", len(uid)) + uid)
+                conns.append((peer, conn))
+            if id_err is not None:
+                raise CommInitError(f"rank 0 could not create the communicator id: {id_err}") from id_err
+            ok, res = _run_with_timeout(init, uid, init_timeout)
+            statuses = [(ok, res if not ok else "")] + [(False, "no report")] * (world - 1)
+            for peer, conn in conns:
+                try:
+                    n = struct.unpack("<I", _recv_exact(conn, 4))[0]
+                    msg = _recv_exact(conn, n).decode(errors="replace")
+                    if 0 < peer < world:
+                        statuses[peer] = (msg == "", msg)
+                except (OSError, ConnectionError) as e:
+                    if 0 < peer < world:
+                        statuses[peer] = (False, f"lost ({e})")
+            good, why = verdict_of(statuses)
+            for _, conn in conns:
+                with contextlib.suppress(OSError):
+                    conn.sendall(struct.pack("<I", len(why.encode())) + why.encode())
         finally:
-            srv.close()
-        return uid
+            for _, conn in conns:
+                conn.close()
+            if srv is not None:
+                srv.close()
+        if not good:
+            raise CommInitError(f"communicator not created on every rank: {why}")
+        return res
     while True:
         try:
-            with socket.create_connection((addr, port), timeout=10) as s:
-                s.sendall(struct.pack("<I", rank))
-                (n,) = struct.unpack("<I", _recv_exact(s, 4))
-                return _recv_exact(s, n)
+            s = socket.create_connection((addr, port), timeout=10)
+            break
         except (ConnectionRefusedError, socket.timeout, OSError) as e:
             if time.monotonic() > deadline:
-                raise RuntimeError(f"rank {rank}: no rendezvous from rank 0 at {addr}:{port} within "
-                                   f"{timeout:.0f} s (BASECOUNT_RDZV_TIMEOUT)") from e
+                raise CommInitError(f"rank {rank}: no rendezvous from rank 0 at {addr}:{port} within "
+                                    f"{timeout:.0f} s (BASECOUNT_RDZV_TIMEOUT)") from e
             time.sleep(0.05)
+    with s:
+        s.settimeout(init_timeout + timeout)
+        try:
+            s.sendall(struct.pack("<I", rank))
+            (n,) = struct.unpack("<I", _recv_exact(s, 4))
+            uid = _recv_exact(s, n)
+        except (OSError, ConnectionError) as e:
+            raise CommInitError(f"rank {rank}: the rendezvous with rank 0 failed ({e})") from e
+        if not uid:
+            raise CommInitError(f"rank {rank}: rank 0 could not create the communicator id")
+        ok, res = _run_with_timeout(init, uid, init_timeout)
+        msg = b"" if ok else (res or "failed").encode()
+        try:
+            s.sendall(struct.pack("<I", len(msg)) + msg)
+            (n,) = struct.unpack("<I", _recv_exact(s, 4))
+            why = _recv_exact(s, n).decode(errors="replace")
+        except (OSError, ConnectionError) as e:
+            raise CommInitError(f"rank {rank}: no verdict from rank 0 ({e})") from e
+    if why:
+        raise CommInitError(f"communicator not created on every rank: {why}")
+    return res
 
 
 class RcclGroup(_GroupOps):
@@ -172,15 +270,18 @@ class RcclGroup(_GroupOps):
             D.check(L.bc_comm_unique_id(buf))
             return bytes(buf)
 
-        uid = rendezvous_id(rank, world, make_id)
-        h = C.c_void_p()
-        ubuf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+        def init(uid):
+            h = C.c_void_p()
+            ubuf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+            D.check(L.bc_comm_init(ctx.h, ubuf, rank, world, C.byref(h)))
+            return h.value
+
         self.world, self.rank = world, rank
         # RCCL prints a version banner on fd 1 when a communicator comes up: keep stdout for the
-        # TSV output (the first collective runs inside the redirect too)
+        # TSV output (the first collective runs inside the redirect too).  The ranks agree on the
+        # outcome (rendezvous_init): either every rank has the communicator or every rank raises.
         with _stdout_to_stderr():
-            D.check(L.bc_comm_init(ctx.h, ubuf, rank, world, C.byref(h)))
-            self.h = h.value
+            self.h = rendezvous_init(rank, world, make_id, init)
             self.barrier()
 
     def barrier(self):

@@ -504,6 +504,9 @@ class _Ungrouped(Exception):
     by reference): start again, accumulating every reference until the end of the file."""
 
 
+_UNGROUPED = object()  # _get_basecounts' answer on every rank when some rank hit _Ungrouped
+
+
 class _ShardMiss(Exception):
     """Sharded decode: this rank's byte range of the file did not hold exactly its references'
     records (file not grouped by reference, or a split the record chain does not confirm)."""
@@ -545,9 +548,12 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
             print(f"basecount[{_group.rank}] sharded decode missed: every rank decodes the file",
                   file=sys.stderr)
     try:
-        return _get_basecounts(*args, grouped=True)
-    except _Ungrouped:
+        res = _get_basecounts(*args, grouped=True)
+    except _Ungrouped:  # (one process: raised where the reference came back)
+        res = _UNGROUPED
+    if res is _UNGROUPED:  # with a group, every rank returns it (the ranks vote after the loop)
         return _get_basecounts(*args, grouped=False)
+    return res
 
 
 def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
@@ -574,6 +580,8 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
         mine = ref_order
         t_lo, t_hi = 0, len(names)  # the refIDs this rank's byte range holds (sharded decode)
         split = set()  # references whose reads several ranks count (their histograms are summed)
+        open_miss = False  # sharded: this rank's range could not be opened
+        ungrouped = False  # with a group: a reference came back after it was finished (this rank)
         if sharded:
             from .dist import BOUND, plan_ranges
 
@@ -596,12 +604,19 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 return find_ref_start(bam, c[0]) if c[1] == BOUND else find_ref_start(bam, c[0], c[1])
 
             with _phase("decode"):
-                beg = where(cuts[rk])
-                end = None if last else where(cuts[rk + 1])
-                if beg is None or (end is not None and end <= beg):
-                    beg = end = None  # no records in this rank's range
                 stream.close()
-                stream = BamStream(bam, voff_range=(beg, end))
+                try:
+                    beg = where(cuts[rk])
+                    end = None if last else where(cuts[rk + 1])
+                    if beg is None or (end is not None and end <= beg):
+                        beg = end = None  # no records in this rank's range
+                    stream = BamStream(bam, voff_range=(beg, end))
+                except (ValueError, OSError):
+                    # a probe or the range open failed on this rank (a damaged block near a cut):
+                    # a miss like any other, so every rank falls back to the whole-file decode,
+                    # which raises the one process's error on every rank
+                    stream = BamStream(bam, voff_range=(None, None))
+                    open_miss = True
         elif _group is not None:
             from .dist import shard
 
@@ -636,6 +651,8 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 raise _ShardMiss() from e
 
         try:
+            if open_miss:
+                raise _ShardMiss()
             with _phase("decode"):
                 cur = next_batch()
             sel_next = None
@@ -733,6 +750,10 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                                                             _mode, tiles_of(ref), _tiles is not None, scratch)
         except _ShardMiss:
             miss = True
+        except _Ungrouped:
+            if _group is None or _group.world == 1:
+                raise
+            ungrouped = True  # told to the other ranks below, before any other collective
         finally:
             for b in (cur, nxt):
                 if b is not None:
@@ -746,7 +767,11 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                 for b in split_acc.values():
                     b.free()
                 return None  # some rank's range did not confirm: every rank decodes the file
-        elif _group is not None and mbq_ok:
+        elif _group is not None:
+            # a file not grouped by reference may show it on some ranks only: all restart together
+            if any(v[0] for v in _group.all_gather_ints([int(ungrouped)])):
+                return _UNGROUPED
+        if not sharded and _group is not None and mbq_ok:
             # every rank needs every reference's first out-of-range read to raise the same error
             flat = [v for r in ref_order for v in fl.range_.get(r, (-2, -1))]
             alls = _group.all_gather_ints(flat)
@@ -880,6 +905,14 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
         bad = ctx.range_error()
         return _empty(k, mode), bad
     scratch = scratch or _Scratch(ctx)
+    if reads.sorted and mode != "rows" and not want_tiles:
+        # --summarise (main.py:469-499 prints six numbers per reference): the summary-only sweep
+        # writes no per-position output, only numpy's buffer partials (bc_pileup_summary)
+        work, dout = scratch.get("work", D.summary_work_bytes(L)), scratch.get("dout", 32)
+        ctx.pileup_summary(reads, L, mbq, k, nf, nf2, None, None, None, None, None, work.ptr, dout.ptr)
+        bad = ctx.range_error()
+        s = dout.download(np.float64, 4)
+        return {"L": L, "avg_cov": np.float64(s[0]), "avg_ent": np.float64(s[1]), "nnz": int(s[2])}, bad
     outs = scratch.outputs(k, L, want_pc=(mode == "rows"))
     hist = scratch.get("hist", 4 * ncols * L)
     pc_ptr = outs["pc"].ptr if outs["pc"] else None

@@ -141,6 +141,24 @@ def make_config(name: str, unsorted: bool = False, contigs=None, reads=None) -> 
                       unsorted=unsorted)
 
 
+def subset(rs: ReadSet, order) -> ReadSet:
+    """The reads of `rs` in the given order (an index array: reorders, drops or repeats records),
+    e.g. a file whose references are interleaved.  Reads are fixed-length (make_reads)."""
+    order = np.asarray(order, np.int64)
+    nc = np.diff(rs.cig_off.astype(np.int64))[order]
+    L = int(rs.seq_off[1] - rs.seq_off[0]) if rs.n else 0
+    Q = int(rs.qual_off[1] - rs.qual_off[0]) if rs.n else 0
+    return ReadSet(references=rs.references, lengths=rs.lengths, tid=rs.tid[order], pos=rs.pos[order],
+                   flag=rs.flag[order], mapq=rs.mapq[order],
+                   cig_off=np.concatenate([[0], np.cumsum(nc)]).astype(np.uint64),
+                   cigar=np.concatenate([rs.cigar[int(rs.cig_off[i]):int(rs.cig_off[i + 1])] for i in order])
+                   if order.size else rs.cigar[:0],
+                   l_seq=rs.l_seq[order], seq_off=(np.arange(order.size + 1) * L).astype(np.uint64),
+                   seq=rs.seq.reshape(rs.n, -1)[order].reshape(-1),
+                   qual_off=(np.arange(order.size + 1) * Q).astype(np.uint64),
+                   qual=rs.qual.reshape(rs.n, -1)[order].reshape(-1), qstart=rs.qstart[order])
+
+
 def write_bam(rs: ReadSet, path: str, level: int = 1) -> None:
     from .bam import write_bam as _w
 

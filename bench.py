@@ -55,9 +55,13 @@ WORKLOADS = {
 KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "solo": "k_pileup_solo (sparse sweep, fused kernel 1 + 2)",
                 "rc": "k_rc (read-chunked kernel 1)",
                 "rc_no_index": "k_rc without the device index (CIGAR words decoded in the kernel)",
+                "rc_indexed": "k_rc from a prebuilt device index (run records + chunk summaries of "
+                              "k_index_runs, replayed; not the step)",
                 "stats": "k_stats (kernel 2)",
                 "index": "k_index_runs + k_index_tiles (the batch's device index, bc_reads_index)",
-                "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)"}
+                "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)",
+                "solo_sum": "k_pileup_solo summary-only sweep (kernels 1 + 2 fused, numpy's partials, no per-position "
+                            "output)"}
 
 
 def read_bytes(b: dict, mbq: int, l_seq: np.ndarray) -> int:
@@ -75,8 +79,11 @@ def kernel_bytes(kernel: str, rb: int, L: int, k: int, with_pc: bool = True) -> 
     entropies; k_rc reads the batch and writes the counts; k_stats reads the counts and writes
     the statistics."""
     stats_out = L * (4 + (8 * k if with_pc else 0) + 16)
+    # the summary-only sweep: the reads, 24 B of partials per 2048-position quarter and the last
+    # partial buffer's coverage + entropy (12 B per position)
+    sum_only = rb + 24 * (L // 2048) + 12 * (L % 8192)
     return {"pileup": rb + 4 * k * L + stats_out, "solo": rb + 4 * k * L + stats_out, "rc": rb + 4 * k * L,
-            "rc_no_index": rb + 4 * k * L, "stats": 4 * k * L + stats_out}[kernel]
+            "rc_no_index": rb + 4 * k * L, "rc_indexed": rb + 4 * k * L, "stats": 4 * k * L + stats_out, "solo_sum": sum_only}[kernel]
 
 
 def lib_sha16() -> str:
@@ -117,33 +124,58 @@ def _loop(fn, budget_s):
             return (time.perf_counter() - t0) / done, done
 
 
-def cpu_baseline(rs, b, L: int, budget_s: float = 10.0) -> dict:
-    """The reference's CPU path on the full C2 workload: its own compiled count.bcount
+def pysam_args(rs, t: int = 0):
+    """The reference's bcount arguments for contig t, as main.py:166-173 builds them from pysam
+    records (all reads accepted, mapq filter 0): query_alignment_sequence (SEQ between the soft
+    clips), query_alignment_qualities, reference_start, cigartuples."""
+    idx = np.flatnonzero(rs.tid == t)
+    nt = np.frombuffer(b"=ACMGRSVTWYHKDBN", np.uint8)
+    reads, quals, starts, ctuples = [], [], [], []
+    for i in idx:
+        n_i = int(rs.l_seq[i])
+        s0 = int(rs.seq_off[i])
+        packed = rs.seq[s0: s0 + (n_i + 1) // 2]
+        codes = np.empty(2 * packed.size, np.uint8)
+        codes[0::2], codes[1::2] = packed >> 4, packed & 15
+        cw = rs.cigar[int(rs.cig_off[i]): int(rs.cig_off[i + 1])]
+        tup = [(int(w) & 15, int(w) >> 4) for w in cw]
+        qs = int(rs.qstart[i])
+        qe = n_i
+        for op, ln in reversed(tup):  # pysam: trailing H skipped, then a trailing S trimmed
+            if op == 5:
+                continue
+            if op == 4:
+                qe -= ln
+            break
+        reads.append(bytes(nt[codes[qs:qe]]).decode())
+        q0 = int(rs.qual_off[i])
+        quals.append(rs.qual[q0 + qs: q0 + qe].tolist())
+        starts.append(int(rs.pos[i]))
+        ctuples.append(tup)
+    return reads, quals, starts, ctuples
+
+
+def cpu_baseline(rs, b, L: int, budget_s: float = 10.0, mbq: int = 0, what: str = "C2", args=None) -> dict:
+    """The reference's CPU path on the full workload: its own compiled count.bcount
     (oracle/_ref, pybind11, Python-list arguments as main.py:146 passes them) + get_stats
-    (main.py:14-79, restated in oracle.get_stats_py).  Single thread, like the reference."""
+    (main.py:14-79, restated in oracle.get_stats_py).  Single thread, like the reference.  The
+    arguments are built once, untimed (pysam's record decode is not part of the timing)."""
     import oracle as O
 
     ref = O.ref_bcount()
     n = int(b["pos"].size)
     if ref is not None:
-        # pysam-shaped arguments (built once, untimed): clipped strings, qualities, starts, tuples
-        seqs = rs.seq.reshape(n, -1)
-        nt = np.frombuffer(b"=ACMGRSVTWYHKDBN", np.uint8)
-        codes = np.empty((n, seqs.shape[1] * 2), np.uint8)
-        codes[:, 0::2], codes[:, 1::2] = seqs >> 4, seqs & 15
-        reads = [bytes(nt[row]).decode() for row in codes]
-        quals = [q for q in rs.qual.reshape(n, -1).tolist()]
-        starts = b["pos"].tolist()
-        ctuples = [[(0, 150)]] * n
-        dt, done = _loop(lambda: O.get_stats_py(ref(L, 0, reads, quals, starts, ctuples), "ref"), budget_s)
-        kind, what = "reference", ("reference count.cpp (pybind11 bcount, list arguments) + "
+        reads, quals, starts, ctuples = args if args is not None else pysam_args(rs, 0)
+        dt, done = _loop(lambda: O.get_stats_py(ref(L, mbq, reads, quals, starts, ctuples), "ref"), budget_s)
+        del reads, quals, starts, ctuples
+        kind, desc = "reference", ("reference count.cpp (pybind11 bcount, list arguments) + "
                                    "get_stats main.py:14-79 (Python)")
     else:
-        dt, done = _loop(lambda: O.stats(O.bcount(L, 0, b)[0], False), budget_s)
-        kind, what = "port", "oracle C restatement of bcount + get_stats"
+        dt, done = _loop(lambda: O.stats(O.bcount(L, mbq, b)[0], False), budget_s)
+        kind, desc = "port", "oracle C restatement of bcount + get_stats"
     return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind, "host": host_info(),
-            "sample": f"{what}; full C2 workload ({n} reads, {L} positions) x {done} runs, "
-                      f"{dt * 1e3:.1f} ms per run, BAM decode excluded"}
+            "sample": f"{desc}; full {what} workload ({n} reads, {L} positions, min_base_quality {mbq}) x "
+                      f"{done} runs, {dt * 1e3:.1f} ms per run, BAM decode excluded"}
 
 
 def cpu_baseline_all_cores(b, L: int, budget_s: float = 5.0) -> dict:
@@ -219,7 +251,7 @@ class Workload:
 
     def __init__(self, ctx, cfg: str, rank: int, world: int, mbq: int, summarise: bool,
                  fused_summary: bool = True, tile_index: bool = True, streams: int = 1,
-                 read_runs: bool = True, copies: int = 1):
+                 read_runs: bool = True, copies: int = 1, summary_only: bool = False):
         from basecount_amd import device as D
         from basecount_amd import synth
         from basecount_amd.bam import seq_to_event
@@ -245,8 +277,11 @@ class Workload:
         self.want_pc = not self.per_contig  # c5 is only ever summarised: no percentages
         self.summarise = summarise
         self.fused_summary = fused_summary
+        # --summarise's step (main.py:469-499 prints six numbers per contig): no per-position output
+        self.summary_only = summary_only and summarise and fused_summary
         self.nf, self.nf2 = norm_factors(self.k)
         self.copies = max(1, int(copies))
+        self.single_pass = not read_runs  # the read-chunked step decodes the raw CIGARs
         self.turn = 0  # the copy the next step reads
         self.work = []
         # bc_reads_upload: host checks + H2D copies + the device index build (run records /
@@ -270,14 +305,17 @@ class Workload:
                 if not tile_index:  # A/B: the tiled kernel searches pos[] (the index stays allocated)
                     r.r.tile_reads = None
                     r.r.n_tiles = 0
-                if not read_runs:  # A/B: the read-chunked kernel decodes the CIGARs itself
+                if not read_runs:  # the read-chunked kernel decodes the CIGARs itself (single pass)
                     r.r.read_runs = None
                 reads.append(r)
             self.h2d_bytes += self.copies * (16 * int(b["pos"].size) + 4 * int(b["cigar"].size) + ev.size)
             k = self.k
-            bufs = dict(counts=ctx.alloc(4 * k * L), cov=ctx.alloc(4 * L),
-                        pc=ctx.alloc(8 * k * L) if self.want_pc else None, ent=ctx.alloc(8 * L),
-                        sec=ctx.alloc(8 * L))
+            if self.summary_only:
+                bufs = dict(counts=None, cov=None, pc=None, ent=None, sec=None)
+            else:
+                bufs = dict(counts=ctx.alloc(4 * k * L), cov=ctx.alloc(4 * L),
+                            pc=ctx.alloc(8 * k * L) if self.want_pc else None, ent=ctx.alloc(8 * L),
+                            sec=ctx.alloc(8 * L))
             if summarise:
                 bufs["swork"] = ctx.alloc(D.summary_work_bytes(L))
             self.work.append((t, L, b, reads, bufs))
@@ -308,7 +346,10 @@ class Workload:
         for i, (_, L, _, reads, o) in enumerate(self.work):
             ctx = self.ctxs[self.on[i]]
             pc = o["pc"].ptr if o["pc"] is not None else None
-            if self.summarise and self.fused_summary:  # kernels 1 + 2 and the summary's partials
+            if self.summary_only:  # kernels 1 + 2 and the summary's partials, nothing per position
+                ctx.pileup_partials(reads[j], L, self.mbq, self.k, self.nf, self.nf2, None, None, None, None,
+                                    None, o["swork"].ptr)
+            elif self.summarise and self.fused_summary:  # kernels 1 + 2 and the summary's partials
                 ctx.pileup_partials(reads[j], L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr,
                                     o["cov"].ptr, pc, o["ent"].ptr, o["sec"].ptr, o["swork"].ptr)
             elif self.summarise:  # kernels 1 + 2, then bc_summary re-reading coverage / entropy
@@ -406,6 +447,22 @@ class Workload:
 
         ok = True
         small = min(self.work, key=lambda w: w[1])
+        if self.summary_only:
+            # no per-position output: the four summary numbers (main.py:469-499), against numpy
+            # over the oracle's coverage / entropies on the smallest contig, and the exact
+            # coverage sum of every contig against the events piled
+            for t, L, b, reads, o in self.work:
+                s = self.d_sum.download(np.float64, 4, offset_bytes=32 * t)
+                if (t, L) == small[:2]:
+                    T = cpu_threads() if 24 * L * cpu_threads() < (2 << 30) else 0
+                    exp, _ = O.bcount(L, self.mbq, b, nthreads=T)
+                    ocov, _, oent, _ = O.stats(exp, False, nthreads=cpu_threads())
+                    ok = ok and s[0] == np.mean(ocov.astype(np.int64)) and s[1] == np.mean(oent)
+                    ok = ok and int(s[2]) == int(np.count_nonzero(ocov))
+                    del exp, ocov, oent
+                if self.mbq == 0 and not self.mixed:
+                    ok = ok and int(s[3]) == synth.ref_events(self.rs, t)
+            return bool(ok)
         for t, L, b, reads, o in self.work:
             if (t, L) == small[:2]:
                 got = o["counts"].download(np.int32, self.k * L).reshape(self.k, L)
@@ -477,14 +534,15 @@ def gather_summaries(group, wl) -> tuple:
 
 
 def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, warmup: int,
-               launch: str, summarise: bool) -> dict:
+               launch: str, summarise: bool, summary_only: bool = False) -> dict:
     """Time K steps of one config (the bench contract: W warmup, barrier + sync on both sides,
     max over ranks) and describe them."""
     from basecount_amd import device as D
 
     copies = args.rotate if args.rotate > 0 else (3 if cfg == "c3" else 1)
     wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused",
-                  args.tile_index == "on", args.streams if summarise else 1, args.read_runs == "on", copies)
+                  args.tile_index == "on", args.streams if summarise else 1, args.read_runs == "on", copies,
+                  summary_only)
     rccl = group is not None and getattr(group, "backend", "") == "rccl"
     gather = None
     if summarise and group is not None:
@@ -525,10 +583,32 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     if ctx.range_error() != -1 or (side is not None and side.range_error() != -1):
         raise RuntimeError(f"{cfg}: out-of-range event in a synthetic batch")
     graph = None
+    trial = None
     if launch == "graph" and gather is None:  # the same K steps, replayed from one captured graph
         graph = ctx.capture((lambda: wl.pipelined(steps, side)) if pipe else (lambda: [step() for _ in range(steps)]))
         graph.launch()  # untimed replay (first-launch setup)
         ctx.sync()
+        if pipe:
+            # Two steps in flight pay a fixed cost per graph launch (the two-stream graph's fork /
+            # join and its nodes' cross-stream dependencies: ~60 us), which a short run
+            # does not amortise.  Both K-step graphs are replayed untimed, alternately, and the
+            # timed region launches the faster one for this K (`launch_trial` in the line).
+            serial_g = ctx.capture(lambda: [step() for _ in range(steps)])
+            serial_g.launch()
+            ctx.sync()
+            best = {"two_in_flight": float("inf"), "serial": float("inf")}
+            for _ in range(3):
+                for name, g in (("two_in_flight", graph), ("serial", serial_g)):
+                    ctx.event_record(2)
+                    g.launch()
+                    ctx.event_record(3)
+                    ctx.sync()
+                    best[name] = min(best[name], ctx.event_elapsed_ms(2, 3) * 1e3 / steps)
+            trial = {k: round(v, 3) for k, v in best.items()}
+            if best["serial"] < best["two_in_flight"]:
+                graph, pipe = serial_g, False
+            else:
+                del serial_g
     if group is not None:
         group.barrier()
     ctx.sync()
@@ -579,7 +659,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
             c.timing(False)
         for name in ("pileup", "solo", "rc", "stats", "summary"):
             if name in rep:
-                kern_s[name] = rep[name] * 1e-6 / reps_t
+                key = "solo_sum" if (name == "solo" and wl.summary_only) else name
+                kern_s[key] = rep[name] * 1e-6 / reps_t
     elif "pileup" in launched or "solo" in launched:
         # eager back-to-back launches: the kernel's own average duration (what rocprofv3's kernel
         # trace reports); a graph replay hides part of the launch gap and would flatter it
@@ -603,17 +684,28 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         if "index" in rep:
             kern_s["index"] = rep["index"][1] * 1e-6
     if "rc" in launched and not summarise and not args.lean:
-        kern_s["rc_no_index"] = region(lambda: wl.count_only("no_index"), reps)
-        # whole steps from the raw batch (index build + k_rc + k_stats), K of them in one graph
+        if wl.single_pass:
+            # the step decodes the CIGARs in k_rc (single pass); beside it, k_rc replaying a device
+            # index built beforehand (each copy's index built once, untimed)
+            for _ in range(wl.copies):
+                wl.rebuild()
+                wl._next()
+            kern_s["rc_indexed"] = region(lambda: wl.count_only("rebuilt"), reps)
+        else:
+            kern_s["rc_no_index"] = region(lambda: wl.count_only("no_index"), reps)
+        # whole steps from the raw batch with the index built first (index build + k_rc + k_stats),
+        # K of them in one graph
         g = ctx.capture(lambda: [wl.raw_step() for _ in range(steps)])
         g.launch()
         ctx.sync()
         ctx.event_record(2)
         g.launch()
         ctx.event_record(3)
-        extra_us["raw_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        extra_us["index_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        if not wl.single_pass:
+            extra_us["raw_step_us"] = extra_us["index_step_us"]
         del g
-    if pipe:
+    if trial is not None:
         # the same K steps serialized on one stream, one graph: the step's own latency
         g = ctx.capture(lambda: [step() for _ in range(steps)])
         g.launch()
@@ -622,6 +714,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         g.launch()
         ctx.event_record(3)
         extra_us["serial_us_per_step"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        if wl.single_pass and "rc" in launched:  # a whole step from the raw batch, serialized
+            extra_us["raw_step_us"] = extra_us["serial_us_per_step"]
         del g
     if side is not None:
         side.sync()
@@ -633,7 +727,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         gather_us = region(gather_step, reps) * 1e6
     wl.step()  # restore the step's outputs (count-only regions accumulated into the counts)
     ctx.sync()
-    dom = max((k for k in kern_s if k in ("pileup", "solo", "rc")), key=kern_s.get)
+    dom = max((k for k in kern_s if k in ("pileup", "solo", "solo_sum", "rc")), key=kern_s.get)
 
     parity = wl.parity()
     if gather is not None and rccl:
@@ -684,6 +778,10 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                       else ", eager launches")
                    + (", two steps in flight (two streams, alternating)" if pipe else ""),
         "steps_in_flight": 2 if pipe else 1,
+        "launch_trial": (None if trial is None else
+                         {"device_us_per_step": trial, "chosen": "two_in_flight" if pipe else "serial",
+                          "what": "both K-step graphs replayed untimed 3x each before the timed region; the "
+                                  "faster one is timed"}),
         "reads_per_rank": int(sum(int(w[2]["pos"].size) for w in wl.work)),
         "positions_per_rank": int(sum(w[1] for w in wl.work)),
         "contigs_per_rank": len(wl.work),
@@ -701,15 +799,38 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                      "algorithmic_bytes": kbytes},
     }
     res.update(extra_us)
-    if "rc_no_index" in kern_s:
+    if "rc_no_index" in kern_s or "rc_indexed" in kern_s:
         nb = wl.bytes_dominant("rc")
-        res["rc_frac_without_index"] = nb / kern_s["rc_no_index"] / 1e9 / HBM_PEAK_GBS
+        single = kern_s["rc"] if wl.single_pass else kern_s["rc_no_index"]
+        res["rc_frac_without_index"] = nb / single / 1e9 / HBM_PEAK_GBS
+        if "rc_indexed" in kern_s:
+            res["rc_frac_indexed_replay"] = nb / kern_s["rc_indexed"] / 1e9 / HBM_PEAK_GBS
         res["index_us"] = kern_s.get("index", 0.0) * 1e6
+        res["step_input"] = ("single pass: k_rc decodes the raw CIGAR words (north_star's input), no index"
+                             if wl.single_pass else "k_rc from the upload's device index (A/B: --read-runs on)")
     if gather_us is not None:
         res["gather_us"] = gather_us
         res["gather_bytes"] = int(gather[0].sum())
     res["_wl"] = wl
     return res
+
+
+def run_c5(ctx, group, args, rank: int, world: int, steps: int, warmup: int, launch: str) -> dict:
+    """C5 as --summarise runs it: the summary-only sweep (no per-position
+    output; main.py:469-499 prints six numbers per contig) is the step; the storing sweep (every
+    count, coverage and entropy written, as the library API, rows and --summarise-with-bed need
+    them) is timed after it on the same contigs and reported beside it as `storing`."""
+    r = run_config("c5", ctx, group, args, rank, world, steps, warmup, launch, summarise=True, summary_only=True)
+    r.pop("_wl").free()
+    s = run_config("c5", ctx, group, args, rank, world, steps, warmup, launch, summarise=True, summary_only=False)
+    wl = s.pop("_wl")
+    r["step"] = "summary only (bc_pileup_partials with no per-position outputs) + one fold"
+    r["storing"] = {k: s[k] for k in ("value", "ms_per_step", "device_us_per_step", "kernel_us", "roofline",
+                                       "parity_vs_oracle") if k in s}
+    r["storing"]["step"] = "counts, coverage and both entropies of every position stored, + partials + fold"
+    r["parity_vs_oracle"] = bool(r["parity_vs_oracle"] and s["parity_vs_oracle"])
+    r["_wl"] = wl
+    return r
 
 
 def run_split(ctx, group, steps: int, warmup: int) -> dict:
@@ -958,8 +1079,9 @@ def main():
                          "then bc_summary per contig (separate)")
     ap.add_argument("--streams", type=int, default=4,
                     help="c5: contexts (streams) the contigs run on concurrently (bc_ctx_wait fork/join)")
-    ap.add_argument("--read-runs", choices=["on", "off"], default="on",
-                    help="off: drop the upload's run records (bc_reads.read_runs), A/B only")
+    ap.add_argument("--read-runs", choices=["on", "off"], default="off",
+                    help="on: the read-chunked step takes the upload's device index (run records + chunk "
+                         "summaries); off (default): the single pass from the raw CIGAR words")
     ap.add_argument("--pipeline", type=int, choices=[1, 2], default=2,
                     help="steps in flight in the timed graph (2: consecutive batches overlap on two "
                          "streams; 1: serialized)")
@@ -1001,18 +1123,23 @@ def main():
     ctx.set_shape(args.shape, args.tile_waves)
     group = None
     if world > 1:
-        from basecount_amd.dist import Group
+        from basecount_amd.dist import CommInitError, Group
 
         try:
             group = Group(ctx=ctx)  # RCCL over xGMI (BASECOUNT_DIST_BACKEND=gloo: rehearsal)
-        except Exception as e:  # noqa: BLE001 - the curve is still measurable over gloo: say so
-            print(f"bench.py rank {rank}: RCCL group failed ({e}); falling back to gloo", file=sys.stderr,
-                  flush=True)
+        except CommInitError as e:
+            # the ranks voted (dist.rendezvous_init): every rank is here, so all of them take gloo;
+            # the line says so (config.comm, config.parallelism, config.comm_fallback)
+            print(f"bench.py rank {rank}: RCCL group failed ({e}); every rank falls back to gloo",
+                  file=sys.stderr, flush=True)
             group = Group("gloo")
             group.fallback = f"rccl failed: {e}"
 
-    head = run_config(args.config, ctx, group, args, rank, world, args.steps, args.warmup, args.launch,
-                      summarise=(args.config == "c5"))
+    if args.config == "c5":
+        head = run_c5(ctx, group, args, rank, world, args.steps, args.warmup, args.launch)
+    else:
+        head = run_config(args.config, ctx, group, args, rank, world, args.steps, args.warmup, args.launch,
+                          summarise=False)
     wl = head.pop("_wl")
     # ---- gather of the per-contig summaries to rank 0 (the output step, after the timed region)
     gather_ms = None
@@ -1039,7 +1166,10 @@ def main():
             if cfg == args.config:
                 continue
             st, wu = (min(args.steps, 200), min(args.warmup, 20)) if cfg != "c5" else (min(args.steps, 10), 2)
-            r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=(cfg == "c5"))
+            if cfg == "c5":
+                r = run_c5(ctx, group, args, rank, world, st, wu, args.launch)
+            else:
+                r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=False)
             r.pop("_wl").free()
             extra[cfg] = r
         if world == 1:
@@ -1068,6 +1198,19 @@ def main():
             b0 = synth.batch_arrays(rs, 0, 0)
             cpu = cpu_baseline(rs, b0, rs.lengths[0], args.cpu_budget)
             cpu_all = cpu_baseline_all_cores(b0, rs.lengths[0], min(5.0, args.cpu_budget))
+            if not args.no_cpu_baseline and "c3" in extra:
+                # the reference at C3 (and with the quality test, mbq 20) beside the
+                # deep kernels; the arguments built once for both
+                import oracle as O
+
+                rs3 = synth.make_config("c3")
+                b3 = synth.batch_arrays(rs3, 0, 0)
+                pa = pysam_args(rs3, 0) if O.ref_bcount() is not None else None
+                budget3 = min(5.0, args.cpu_budget)
+                extra["c3"]["cpu_baseline"] = cpu_baseline(rs3, b3, rs3.lengths[0], budget3, 0, "C3", pa)
+                if "c3_q20" in extra:
+                    extra["c3_q20"]["cpu_baseline"] = cpu_baseline(rs3, b3, rs3.lengths[0], budget3, 20, "C3", pa)
+                del pa, b3, rs3
         if not args.no_e2e and args.config == "c2":
             e2e_res = e2e("c2")
             if not args.no_extras:  # the other shapes' CLI paths too
@@ -1093,7 +1236,8 @@ def main():
                        "positions_per_rank": head["positions_per_rank"],
                        "contigs_per_rank": head["contigs_per_rank"], "min_base_quality": args.mbq,
                        "percentages_stored": args.config != "c5",
-                       "parallelism": f"contig-sharded x{world}",
+                       "parallelism": f"contig-sharded x{world}"
+                                      + (f" over {group.backend}" if group is not None else ""),
                        "comm": (group.backend if group is not None else None),
                        "comm_fallback": getattr(group, "fallback", None),
                        "shape": args.shape, "tile_waves": args.tile_waves,
@@ -1115,6 +1259,7 @@ def main():
         if "gather_us" in head:
             line["gather_us"] = head["gather_us"]
         line["steps_in_flight"] = head["steps_in_flight"]
+        line["launch_trial"] = head.get("launch_trial")
         if "serial_us_per_step" in head:
             line["serial_us_per_step"] = head["serial_us_per_step"]
         if cpu:

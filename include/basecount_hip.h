@@ -300,7 +300,13 @@ int bc_pileup_summary(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uin
  * partial sums of one reference in d_work; bc_summary_fold then folds n references' partials
  * (one workgroup each, side by side: the fold is one dependent add per 8192 positions, the only
  * sequential step of the summary) and writes each reference's 4 doubles to d_outs[i].
- * ref_lens / d_works / d_outs are host arrays of n entries (device pointers).                  */
+ * ref_lens / d_works / d_outs are host arrays of n entries (device pointers).
+ * Summary only: with d_counts, d_cov, d_pc, d_ent and d_sec ALL NULL, bc_pileup_partials (and
+ * bc_pileup_summary) write no per-position output (the CLI's --summarise prints six numbers per
+ * reference): a sparse batch's sweep writes only the summary partials (and the coverage /
+ * entropy of the last partial 8192-position buffer, into context scratch); other batches write
+ * their outputs into context scratch.  Same numbers, bit for bit.  The scratch grows on first use
+ * (a synchronizing allocation: make that call outside a graph capture).                        */
 int bc_pileup_partials(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality, int k,
                        double nf, double nf2, int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent,
                        double* d_sec, void* d_work);

@@ -137,3 +137,58 @@ def test_cli_world2_same_error_as_single_process(tmp_path):
     strip = lambda line: line.split("]: ", 1)[1] if line.startswith("[rank") else line  # noqa: E731
     assert s_err[0].startswith("ZeroDivisionError") and strip(m_err[0]) == s_err[0]
     assert m_out == s_out
+
+
+def _comm_worker(path, fail_rank, fail_what):
+    # run by subprocess: the communicator vote with stand-ins for the RCCL id and init
+    import time
+
+    from basecount_amd.dist import CommInitError, env, rendezvous_init
+
+    world, rank, _ = env()
+
+    def make_id():
+        if fail_what == "id" and rank == fail_rank:
+            raise RuntimeError("no id")
+        return bytes(range(128))
+
+    def init(uid):
+        assert uid == bytes(range(128))
+        if fail_what == "init" and rank == fail_rank:
+            raise RuntimeError("init refused")
+        if fail_what == "hang" and rank == fail_rank:
+            time.sleep(600)
+        return 1000 + rank
+
+    t0 = time.monotonic()
+    try:
+        res = repr(rendezvous_init(rank, world, make_id, init, timeout=30, init_timeout=3))
+    except CommInitError as e:
+        res = "CommInitError: " + str(e)
+    with open(f"{path}.{rank}", "w") as fh:
+        fh.write(f"{time.monotonic() - t0:.1f} {res}")
+
+
+@pytest.mark.parametrize("fail_rank,fail_what", [(None, None), (1, "init"), (0, "init"), (0, "id"),
+                                                 (1, "hang")])
+def test_comm_init_is_agreed_by_every_rank(tmp_path, fail_rank, fail_what):
+    """the RCCL group comes up on every rank or on none.  A failing (or hung)
+    init on one rank makes every rank raise CommInitError within seconds, so the bench's gloo
+    fallback is taken by all ranks alike instead of leaving some in a collective."""
+    world = 3
+    path = tmp_path / "c"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+               BASECOUNT_RDZV_PORT=str(_free_port()))
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import test_dist as t; "
+            "t._comm_worker(%r, %r, %r)" % (os.path.dirname(HERE), HERE, str(path), fail_rank, fail_what))
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
+             for r in range(world)]
+    assert [p.wait(timeout=120) for p in procs] == [0] * world
+    res = [(tmp_path / f"c.{r}").read_text().split(" ", 1) for r in range(world)]
+    assert all(float(t) < 20 for t, _ in res)
+    if fail_rank is None:
+        assert [r for _, r in res] == [repr(1000 + r) for r in range(world)]
+    else:
+        assert all(r.startswith("CommInitError") for _, r in res), res
+        if fail_what != "id":
+            assert all(f"rank {fail_rank}" in r for _, r in res), res

@@ -94,6 +94,35 @@ def test_c5_contig(ctx, c5, c5_event, t):
         r.free()
 
 
+def test_c5_summary_only_per_contig(ctx, c5, c5_event):
+    """the summary-only sweep (bc_pileup_summary with no per-position outputs,
+    what --summarise needs) on every C5 contig: the same four numbers as numpy over the oracle's
+    per-position coverage and entropies (main.py:469-499)."""
+    k = 5
+    nf, nf2 = norm_factors(k)
+    for t, name in enumerate(c5.references):
+        L = c5.lengths[t]
+        b = synth.batch_arrays(c5, t, 0)
+        r = D.DeviceReads(ctx, dict(b, seq_event=c5_event))
+        work, out = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        try:
+            ctx.pileup_summary(r, L, 0, k, nf, nf2, None, None, None, None, None, work.ptr, out.ptr)
+            assert ctx.range_error() == -1
+            s = out.download(np.float64, 4)
+            exp, (br, _) = O.bcount(L, 0, b)
+            assert br == -1
+            ocov, _, oent, _ = O.stats(exp, False, nthreads=T)
+            del exp
+            # main.py:469-499's numbers: np.mean of the coverages and entropies, the covered count
+            assert s[0] == np.mean(ocov.astype(np.int64)) and s[1] == np.mean(oent), name
+            assert int(s[2]) == int(np.count_nonzero(ocov)) and int(s[3]) == int(ocov.sum(dtype=np.int64))
+            del ocov, oent
+        finally:
+            work.free()
+            out.free()
+            r.free()
+
+
 @pytest.mark.parametrize("batch", [None, "200000"])
 def test_c5_cli_summarise(c5, tmp_path, monkeypatch, batch):
     """batch 200000: the 1.2 M records stream in 6 batches; contigs cut by a batch boundary are

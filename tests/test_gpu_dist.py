@@ -275,3 +275,47 @@ def test_split_reference_cli_matches_one_process(single_contig_bams, tmp_path, w
         else:
             assert all(r != 0 for r in rcn), (args, rcn)
             assert _last_line(errn[0]) == _last_line(err1[0]), (args, errn[0][-800:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shard_decode", ["0", "1"])
+def test_ungrouped_file_restarts_on_every_rank(tmp_path, shard_decode):
+    """a file not grouped by reference (A..., B..., A...) makes only the rank owning A
+    see A come back; the ranks vote after the batch loop and all restart in accumulate mode
+    together (a per-rank restart desynchronised their collectives).  With the sharded decode the
+    ranges miss and every rank decodes the whole file.  Output identical to one process."""
+    from basecount_amd import synth
+
+    rs = synth.make_reads([("A", 6_000), ("B", 4_000)], 6_000, True, 31)
+    # the file order: A's first half, all of B, A's second half (each part coordinate-sorted)
+    ia, ib = np.flatnonzero(rs.tid == 0), np.flatnonzero(rs.tid == 1)
+    order = np.concatenate([ia[: ia.size // 2], ib, ia[ia.size // 2:]])
+    bam = str(tmp_path / "aba.bam")
+    synth.write_bam(synth.subset(rs, order), bam)
+    for args in ([], ["--summarise"]):
+        rc1, out1, err1 = _ranks(1, [bam, *args], tmp_path, "one")
+        env = {"BASECOUNT_SHARD_DECODE": shard_decode, "BASECOUNT_BATCH_RECORDS": "1500"}
+        rc2, out2, err2 = _ranks(2, [bam, *args], tmp_path, "two", env)
+        assert rc1 == [0] and rc2 == [0, 0], (err1[0][-1500:], [e[-1500:] for e in err2])
+        assert out2 == out1 and len(out1) > 100
+
+
+@pytest.mark.gpu
+def test_damaged_block_near_a_cut_fails_every_rank_alike(shard_bams, tmp_path):
+    """with the sharded decode, a damaged BGZF block near a rank's cut used to fail the
+    probe (or the range open) on that rank only while the others waited in the shard merge.  Now
+    it is a miss on that rank, every rank decodes the whole file and raises the one process's
+    error."""
+    ok, _ = shard_bams
+    data = bytearray(open(ok, "rb").read())
+    for frac in (0.35, 0.5, 0.65):
+        at = int(len(data) * frac)
+        bad = bytearray(data)
+        bad[at: at + 96] = bytes(range(96))
+        path = str(tmp_path / f"damaged{frac}.bam")
+        open(path, "wb").write(bad)
+        rc1, out1, err1 = _ranks(1, [path], tmp_path, f"one{frac}")
+        rc2, out2, err2 = _ranks(2, [path], tmp_path, f"two{frac}")
+        assert rc1[0] != 0, "the damaged file decoded"
+        assert all(r != 0 for r in rc2), rc2
+        assert _last_line(err2[0]) == _last_line(err1[0]), (err2[0][-800:], err1[0][-800:])

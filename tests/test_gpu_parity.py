@@ -727,11 +727,13 @@ def test_full_size_configs_exact(ctx, cfg, mmq, mbq, path):
         assert int(got.sum()) + int(exp[:, 5].sum()) == synth.ref_events(rs)
 
 
-@pytest.mark.parametrize("path", ["auto", "tile", "rc"])
-def test_full_size_c3_fused_pileup(ctx, path):
-    """The bench's step (bc_pileup) on the full C3 batch: counts exact, stats within 1e-6."""
+@pytest.mark.parametrize("cfg,path", [("c3", "auto"), ("c3", "tile"), ("c3", "rc"), ("c2", "auto")])
+def test_full_size_fused_pileup(ctx, cfg, path):
+    """The bench's step (bc_pileup) on the full C3 batch, and on the full C2 batch (the
+    headline's fused k_pileup with statistics): counts, coverage and
+    percentages exact, entropies bit-identical (and within north_star's 1e-6)."""
     ctx.set_shape(path)
-    rs = synth.make_config("c3")
+    rs = synth.make_config(cfg)
     b = synth.batch_arrays(rs, 0, 0)
     L = rs.lengths[0]
     exp, (br, _) = O.bcount(L, 0, b)
@@ -741,6 +743,35 @@ def test_full_size_c3_fused_pileup(ctx, path):
     ocov, opc, oent, osec = O.stats(exp, False)
     assert np.array_equal(cov, ocov) and np.array_equal(pc, opc)
     assert np.max(np.abs(ent - oent)) <= 1e-6 and np.max(np.abs(sec - osec)) <= 1e-6
+    assert np.array_equal(ent, oent) and np.array_equal(sec, osec)
+
+
+@pytest.mark.parametrize("mbq,ncols", [(0, 5), (20, 6)])
+def test_rc_64bit_indices_chromosome_scale(ctx, mbq, ncols):
+    """k_rc's int64_t instantiation (taken when L or n >= 2^27, i.e. deep
+    batches on human chr1-chr12 / X) against the oracle: L = 2^27 + 10,000, 20,000 mixed-CIGAR
+    reads near the far end and a few at 0, shape forced to rc; then the same batch with the
+    reference cut short, whose first offending read must be the oracle's (count.cpp:17,60-65)."""
+    ctx.set_shape("rc")
+    L = (1 << 27) + 10_000
+    rng = np.random.default_rng(77 + mbq)
+    b = shaped_batch(rng, 20_000, 20_000, IMAGE_DEEP + FALLBACK)
+    far = np.arange(b["pos"].size) >= 40  # the 40 leftmost reads stay near position 0
+    b["pos"] = (b["pos"].astype(np.int64) + np.where(far, L - 20_000, 0)).astype(np.int32)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    got, bad = gpu_count(ctx, b, L, mbq, ncols)
+    assert bad == -1
+    exp = exp[:, :ncols]
+    assert int(got.sum(dtype=np.int64)) == int(exp.sum(dtype=np.int64))
+    for lo, hi in ((0, 20_000), (L - 20_000, L)):
+        assert np.array_equal(got[:, lo:hi], exp[lo:hi].T.astype(np.int32)), (lo, hi)
+    del got, exp
+    L2 = L - 60  # reads now run past the end: std::out_of_range in the reference
+    _, (br2, _) = O.bcount(L2, mbq, b)
+    assert br2 >= 0
+    _, bad2 = gpu_count(ctx, b, L2, mbq, ncols)
+    assert bad2 == br2
 
 
 @pytest.mark.parametrize("L,n,mbq,show_n", [
@@ -780,6 +811,38 @@ def test_pileup_summary_matches_separate_calls(ctx, L, n, mbq, show_n):
     cov, ent, s = outs[1][1], outs[1][2], outs[1][4]
     assert s[0] == np.mean(cov.astype(np.int64)) and s[1] == np.mean(ent)
     assert int(s[2]) == int(np.count_nonzero(cov)) and int(s[3]) == int(cov.astype(np.int64).sum())
+    # summary only: no per-position outputs at all, the same four doubles
+    work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+    for rep in range(2):  # (the second call reuses the context's tail scratch)
+        work.zero()
+        ctx.pileup_summary(r, L, mbq, k, nf, nf2, None, None, None, None, None, work.ptr, dout.ptr)
+        assert ctx.range_error() == -1
+        assert np.array_equal(dout.download(np.float64, 4), s), rep
+
+
+@pytest.mark.parametrize("L,n", [(8192 * 40 + 3_000, 30), (8192 * 3, 0), (5_000_000, 200)])
+def test_pileup_summary_only_sparse_edges(ctx, L, n):
+    """The summary-only sweep on read-free quarters (one constant store each), a batch with no
+    reads, and a reference whose last buffer is partial: the summary equals numpy's over the
+    storing call's arrays."""
+    rng = np.random.default_rng(L + 7)
+    b = random_batch(rng, L, n) if n else random_batch(rng, L, 1)
+    if not n:
+        b = dict(b, pos=b["pos"][:0], cig_beg=b["cig_beg"][:0], cig_n=b["cig_n"][:0], seq_nib=b["seq_nib"][:0])
+    k = 5
+    nf, nf2 = norm_factors(k)
+    r = D.DeviceReads(ctx, b)
+    bufs = [ctx.alloc(max(8, x)) for x in (4 * k * L, 4 * L, 8 * L, 8 * L)]
+    work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+    ctx.pileup_summary(r, L, 0, k, nf, nf2, bufs[0].ptr, bufs[1].ptr, None, bufs[2].ptr, bufs[3].ptr,
+                       work.ptr, dout.ptr)
+    want = dout.download(np.float64, 4)
+    cov, ent = bufs[1].download(np.int32, L), bufs[2].download(np.float64, L)
+    assert want[0] == np.mean(cov.astype(np.int64)) and want[1] == np.mean(ent)
+    work.zero()
+    ctx.pileup_summary(r, L, 0, k, nf, nf2, None, None, None, None, None, work.ptr, dout.ptr)
+    assert ctx.range_error() == -1
+    assert np.array_equal(dout.download(np.float64, 4), want)
 
 
 def test_summary_fold_many_references(ctx):

@@ -55,16 +55,17 @@ def test_bench_world_size_must_match_gpus():
 _RDZV = """
 import sys
 sys.path.insert(0, {repo!r})
-from basecount_amd.dist import rendezvous_id
+from basecount_amd.dist import rendezvous_init
 rank, world = int(sys.argv[1]), int(sys.argv[2])
-uid = rendezvous_id(rank, world, lambda: bytes(range(128)) if rank == 0 else None, timeout=60)
+# init: the id itself (the RCCL communicator's stand-in)
+uid = rendezvous_init(rank, world, lambda: bytes(range(128)), lambda u: u, timeout=60)
 sys.stdout.write(uid.hex())
 """
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_rendezvous_id_every_rank_gets_rank0s_bytes(world):
-    """dist.rendezvous_id: rank 0's id reaches every rank (the RCCL id handshake, without RCCL)."""
+    """dist.rendezvous_init: rank 0's id reaches every rank (the RCCL id handshake, without RCCL)."""
     env = _env(MASTER_ADDR="127.0.0.1", BASECOUNT_RDZV_PORT=str(_free_port()))
     code = _RDZV.format(repo=REPO)
     # the non-root ranks start first: they must wait for the root's socket

@@ -449,6 +449,7 @@ int bc_reads_sort(bc_ctx* c, const bc_reads* r, bc_reads* out, void* d_mem, size
     uint32_t overflow = 0;
     HIP_TRY(hipMemcpyAsync(&overflow, bc::sort_overflow_word(*r, d_mem), 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (overflow & 2u) return fail(BC_E_ARG, "bc_reads_sort: a read starts outside [0, max_end] (max_end not truthful)");
     if (overflow) return fail(BC_E_ARG, "bc_reads_sort: the reads' sequences overlap (sorted copy would not fit)");
     *out = tmp;
     return BC_OK;

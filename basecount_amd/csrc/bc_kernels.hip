@@ -265,8 +265,15 @@ __global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, in
                                                    double* __restrict__ sec) {
     __shared__ int32_t cnt[K][64];
     __shared__ double t1[K][64], t2[K][64];
+    // glibc log2's table copied to LDS with the first loads, so that each term's table lookup
+    // is an LDS read instead of a dependent global round trip (kernel 2 is one tile deep: its
+    // time is its chain of round trips)
+    __shared__ __attribute__((aligned(16))) double tab[64][4];
     const int j = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t n_tiles = (L + 63) / 64;
+    if (threadIdx.x < 128)
+        *(double2*)&tab[threadIdx.x >> 1][2 * (threadIdx.x & 1)] =
+            *(const double2*)&log2d::kTab[threadIdx.x >> 1][2 * (threadIdx.x & 1)];
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int64_t p = tile * 64 + lane;
         const bool in = p < L;
@@ -295,11 +302,11 @@ __global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, in
         if (in && cov != 0) {
             const double pj = (double)cj / (double)cov;
             if (pc) pc[(int64_t)j * L + p] = 100.0 * pj;
-            if (cj != 0) e1 = -(pj * glibc_log2(pj));
+            if (cj != 0) e1 = -(pj * glibc_log2_t(pj, tab));
             const int64_t cov2 = cov - c[am];
             if (sec && j != am && cj != 0 && cov2 != 0) {
                 const double q = (double)cj / (double)cov2;
-                e2 = -(q * glibc_log2(q));
+                e2 = -(q * glibc_log2_t(q, tab));
             }
         } else if (in && pc) {
             pc[(int64_t)j * L + p] = -1.0;

@@ -25,8 +25,13 @@
 
 namespace bc {
 
-BC_LOG2_HD double glibc_log2(double x) {
-    using namespace log2d;
+// TAB: the (invc, logc, chi, clo) table, indexable as tab[i][j] (log2d::kTab, or a copy in LDS)
+template <typename TAB>
+BC_LOG2_HD double glibc_log2_t(double x, const TAB& kTab) {
+    using log2d::kA;
+    using log2d::kB;
+    using log2d::kInvLn2Hi;
+    using log2d::kInvLn2Lo;
     const uint64_t ix = __builtin_bit_cast(uint64_t, x);
     if (ix - 0x3feea4af00000000ull < 0x3ff0b55900000000ull - 0x3feea4af00000000ull) {
         // close to 1.0: log2(1 + r) by the second polynomial, r exact
@@ -64,5 +69,7 @@ BC_LOG2_HD double glibc_log2(double x) {
     const double p = kA[0] + r * kA[1] + r2 * (kA[2] + r * kA[3]) + r4 * (kA[4] + r * kA[5]);
     return lo + r2 * p + hi;
 }
+
+BC_LOG2_HD double glibc_log2(double x) { return glibc_log2_t(x, log2d::kTab); }
 
 }  // namespace bc

@@ -139,6 +139,7 @@ struct SortArgs {
     uint8_t* o_qual;
     uint32_t cap;       // bytes of o_seq (o_qual: twice as many)
     int64_t qual_bytes;
+    int64_t nbins;      // bins: starts in [0, nbins - 1)
 };
 
 // read i: its rank inside its start's bin (one atomic on the bin), its query length from the
@@ -147,7 +148,11 @@ struct SortArgs {
 __global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= A.n) return;
-    const int32_t pos = A.pos[i];
+    int32_t pos = A.pos[i];
+    if (pos < 0 || (int64_t)pos >= A.nbins - 1) {  // a start outside [0, max_end]: the caller's batch is wrong
+        atomicOr(A.overflow, 2u);                     // (bc_reads_sort returns BC_E_ARG)
+        pos = 0;
+    }
     const uint32_t cb = A.cig_beg[i], cn = A.cig_n[i], sn = A.seq_nib[i];
     const uint32_t rank = atomicAdd(&A.bins[pos], 1u);
     const uint32_t* cg = A.cigar + cb;
@@ -294,6 +299,7 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     A.o_qual = r.qual ? b + L.o_qual : nullptr;
     A.cap = L.cap;
     A.qual_bytes = r.qual ? r.qual_bytes : 0;
+    A.nbins = L.nbins;
     uint32_t* tmp = (uint32_t*)(b + L.tmp);
     const unsigned blocks = (unsigned)((r.n_reads + 255) / 256);
     hipError_t e = hipMemsetAsync(A.bins, 0, 4 * (size_t)L.nbins, s);

@@ -244,7 +244,8 @@ def _scratch(ctx) -> _Scratch:
 
 
 def release_device_memory() -> None:
-    """Free the HBM the CLI / library calls keep for reuse (batch buffers, outputs)."""
+    """Free the HBM kept for reuse by the CLI and by library calls made with _keep_scratch
+    (batch buffers, outputs); get_basecounts / BaseCount release their own when they return."""
     for sc in _SCRATCHES.values():
         sc.release()
     _SCRATCHES.clear()
@@ -520,7 +521,7 @@ def _shard_decode_on(group) -> bool:
 
 def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality=0,
                    chunk_size=1000000, show_n_bases=False, long_format=False, *, device=None,
-                   _mode="rows", _tiles=None, _group=None):
+                   _mode="rows", _tiles=None, _group=None, _keep_scratch=False):
     """main.py:110-205 on the device.  Returns {ref: {"rows": Rows, "num_reads": n}} in the
     reference's (set) order.  ``_mode="summary"`` keeps per-position data in HBM and returns
     the numpy-exact summary (and amplicon) reductions instead of rows.
@@ -533,7 +534,21 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
 
     With ``_group`` (a dist.Group, one process per GPU) the references are sharded over the
     ranks (dist.shard): this rank computes and returns only the ones it owns, and the function
-    returns ``(results, owner, order)``; every rank raises the same first error."""
+    returns ``(results, owner, order)``; every rank raises the same first error.
+
+    Device memory: the call's HBM scratch (batch buffers, outputs; the results are on the host)
+    is released when it returns, unless it runs inside the CLI (run(), one process per command)
+    or ``_keep_scratch`` asks to keep it for the next call (release_device_memory() frees it)."""
+    try:
+        return _get_basecounts_top(bam, references, min_base_quality, min_mapping_quality, chunk_size,
+                                   show_n_bases, long_format, device, _mode, _tiles, _group)
+    finally:
+        if _DEFERRED is None and not _keep_scratch:
+            release_device_memory()
+
+
+def _get_basecounts_top(bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
+                        long_format, device, _mode, _tiles, _group):
     args = (bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
             long_format, device, _mode, _tiles, _group)
     if _shard_decode_on(_group):

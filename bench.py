@@ -219,7 +219,7 @@ def e2e(cfg: str, summarise: bool = False) -> dict:
             f.select(0, [True] * len(f.references))
 
     def pipeline():
-        data = M.get_basecounts(bam, _mode="summary" if summarise else "rows")
+        data = M.get_basecounts(bam, _mode="summary" if summarise else "rows", _keep_scratch=True)
         if not summarise:
             for ref, v in data.items():
                 d = v["rows"].d
@@ -752,7 +752,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     pmc = os.path.join(REPO, "profiles", "kernel1_pmc.json")
     if os.path.exists(pmc) and world == 1:
         with open(pmc) as fh:
-            pm = json.load(fh).get(cfg, {})
+            pm = json.load(fh).get(cfg if args.mbq == 0 else f"{cfg}_q{args.mbq}", {})
         if (pm and pm.get("mbq", 0) == args.mbq and pm.get("kernel", "pileup") == dom
                 and pm.get("lib_sha16") == lib_sha16() and pm.get("copies", 1) == copies):
             traffic = pm.get("hbm_bytes_per_launch")

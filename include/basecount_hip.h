@@ -104,7 +104,10 @@ typedef struct bc_reads {
      * a hash of n_reads, sorted, max_span, max_end and the pos / cig_beg pointers.  The kernels
      * use tile_reads / read_runs only while it matches, so a copied struct that was sliced (pos
      * offset, n_reads shrunk) or given another max_span falls back to searching / decoding
-     * instead of reading another batch's index.  0 = no index.                              */
+     * instead of reading another batch's index.  0 = no index.
+     * The tag detects slicing, not new CONTENT in the same buffers: a caller that refills the
+     * arrays of a struct in place (same pointers, same counts and bounds) must set index_tag = 0
+     * or rebuild the index (bc_reads_index) before the next launch.                          */
     uint64_t index_tag;
 } bc_reads;
 
@@ -182,7 +185,8 @@ int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
  * bc_reads_index) that every kernel takes, with the same counts as the input (count.cpp's sums
  * do not depend on the read order).  Needs d_reads->max_end truthful and seq_layout ==
  * BC_SEQ_EVENT; the reads' aligned sequences must not overlap (true of any decoded batch).
- * Blocking: returns after the copy is complete (BC_E_ARG if the sequences did overlap).      */
+ * Blocking: returns after the copy is complete (BC_E_ARG if the sequences did overlap, or if a
+ * read starts outside [0, max_end]: device starts are checked, not trusted).                 */
 int bc_reads_sort_bytes(bc_ctx* ctx, const bc_reads* d_reads, size_t* bytes);
 int bc_reads_sort(bc_ctx* ctx, const bc_reads* d_reads, bc_reads* d_sorted, void* d_mem, size_t bytes);
 

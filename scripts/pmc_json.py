@@ -5,7 +5,8 @@ MI355X_MICROARCH.md prescribes for gfx950: (2 x FETCH_SIZE + WRITE_SIZE) KiB.
     python scripts/pmc_json.py profiles/r03_pmc.json profiles/kernel1_pmc.json \\
         c2=gpurun_out/pmc_c2:k_pileup:pileup:1 c3=gpurun_out/pmc_c3:k_rc:rc:3 c5=gpurun_out/pmc_c5:k_pileup_solo:solo:1:24
 
-Each spec is dir:kernel-name-substring:bench-kernel-key:batch-copies[:launches-per-step].  The
+Each spec is dir:kernel-name-substring:bench-kernel-key:batch-copies[:launches-per-step[:mbq]]
+(name c3_q20 for the C3 run at --mbq 20: bench.py looks entries up as <config>[_q<mbq>]).  The
 second file is what bench.py reads as roofline.traffic: it carries the sha of the library the
 counters were read from (bench.py reports traffic null for any other build).
 """
@@ -50,10 +51,11 @@ def main():
         parts = spec.split(":")
         d, pat, key, copies = parts[0], parts[1], parts[2], int(parts[3])
         per_step = int(parts[4]) if len(parts) > 4 else 1
+        mbq = int(parts[5]) if len(parts) > 5 else 0
         s = summarise(d, pat)
         full[name] = dict(kernel=pat, **s)
         if "hbm_bytes_per_launch" in s:
-            traffic[name] = {"mbq": 0, "kernel": key, "copies": copies, "lib_sha16": sha,
+            traffic[name] = {"mbq": mbq, "kernel": key, "copies": copies, "lib_sha16": sha,
                              "fetch_size_kib": s["FETCH_SIZE"], "write_size_kib": s["WRITE_SIZE"],
                              "hbm_bytes_per_launch": s["hbm_bytes_per_launch"] * per_step,
                              "dispatches": s["dispatches"], "launches_per_step": per_step}

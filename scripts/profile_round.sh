@@ -6,14 +6,16 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-for c in ${CFGS:-c2 c3 c5}; do
-  steps=200; extra=""; [ "$c" = c5 ] && steps=5 && extra="--streams 1"  # c5: launches serialized, so their durations add up
+for c in ${CFGS:-c2 c3 c5 c3q20}; do
+  steps=200; extra=""; cfg=$c
+  [ "$c" = c5 ] && steps=5 && extra="--streams 1"  # c5: launches serialized, so their durations add up
+  [ "$c" = c3q20 ] && cfg=c3 && extra="--mbq 20"   # C3 with the quality test (QUAL bytes read)
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$c -o run -- \
-    python bench.py --config $c --no-cpu-baseline --no-extras --no-e2e --lean --launch eager --steps $steps --warmup 2 $extra \
+    python bench.py --config $cfg --no-cpu-baseline --no-extras --no-e2e --lean --launch eager --steps $steps --warmup 2 $extra \
     > gpurun_out/prof_$c.log 2>&1
   rc=$?; echo "trace $c rc=$rc"; fatal $rc && exit $rc
-  passes="4 5"; [ "$c" != c5 ] && passes="1 2 3 4 5"
-  PASSES="$passes" BENCH_ARGS="--config $c" OUT=pmc_$c bash scripts/pmc.sh
+  passes="4 5"; [ "$c" = c2 ] || [ "$c" = c3 ] && passes="1 2 3 4 5"
+  PASSES="$passes" BENCH_ARGS="--config $cfg $([ "$c" = c3q20 ] && echo --mbq 20)" OUT=pmc_$c bash scripts/pmc.sh
   rc=$?; fatal $rc && exit $rc
 done
 echo PROFILES_DONE

@@ -565,7 +565,8 @@ int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, in
         // scratch); the other paths write their outputs into context scratch.
         if (k != 5 && k != 6) return fail(BC_E_ARG, "k must be 5 or 6");
         DeviceGuard g(c->device);
-        if (sparse_path && L >= bc::kNpBuf) {
+        // (the sparse sweep k_pileup_solo is the kernel that fuses the partials)
+        if (sparse_path && L >= bc::kNpBuf && bc::pileup_is_solo(*r, L, c->shape, c->tile_waves)) {
             if (!r->sorted) return fail(BC_E_ARG, "bc_pileup needs a coordinate-sorted batch (sorted == 1)");
             if (mbq > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
             if (r->seq_layout != BC_SEQ_EVENT) return fail(BC_E_ARG, "bc_pileup needs seq_layout == BC_SEQ_EVENT");

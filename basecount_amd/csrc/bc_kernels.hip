@@ -338,6 +338,72 @@ __global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, in
     }
 }
 
+// Kernel 2 with one lane per position (all K columns in the lane, the terms independent so they
+// overlap) and no block barrier but the table copy's: a launch of ~L / 256 blocks whose chain is
+// the counts' load (issued before the table copy, so both are in flight together), the fp64
+// terms and the stores.  The arithmetic is bc_stats.h's position_stats (the fused kernels'), so the
+// results are those of k_stats bit for bit; NULL cov / pc / ent / sec are skipped as in k_stats.
+template <int K>
+__global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, int64_t L, double nf, double nf2,
+                                                    int32_t* __restrict__ counts_out, int32_t* __restrict__ cov_out,
+                                                    double* __restrict__ pc, double* __restrict__ ent,
+                                                    double* __restrict__ sec) {
+    __shared__ __attribute__((aligned(16))) double tab[64][4];
+    const int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool in = P < L;
+    uint32_t c[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) c[j] = in ? (uint32_t)hist[(int64_t)j * L + P] : 0u;
+    if (threadIdx.x < 128)
+        *(double2*)&tab[threadIdx.x >> 1][2 * (threadIdx.x & 1)] =
+            *(const double2*)&log2d::kTab[threadIdx.x >> 1][2 * (threadIdx.x & 1)];
+    __syncthreads();
+    if (!in) return;
+    if (counts_out) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            counts_out[(int64_t)j * L + P] = (int32_t)c[j];
+            hist[(int64_t)j * L + P] = 0;
+        }
+    }
+    int64_t cov = 0;
+    int am = 0;
+    uint32_t mx = c[0];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        cov += c[j];
+        if (c[j] > mx) mx = c[j], am = j;  // np.argmax: first maximum
+    }
+    if (cov_out) cov_out[P] = (int32_t)cov;
+    double h = 1.0, h2 = 1.0;
+    if (cov != 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const double pj = (double)c[j] / (double)cov;
+            if (pc) pc[(int64_t)j * L + P] = 100.0 * pj;
+            if (c[j] != 0) s = s + (-(pj * glibc_log2_t(pj, tab)));
+        }
+        h = nf * s;
+        const int64_t cov2 = cov - (int64_t)mx;
+        if (cov2 != 0 && sec) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (j != am && c[j] != 0) {
+                    const double q = (double)c[j] / (double)cov2;
+                    s2 = s2 + (-(q * glibc_log2_t(q, tab)));
+                }
+            h2 = nf2 * s2;
+        }
+    } else if (pc) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) pc[(int64_t)j * L + P] = -1.0;
+    }
+    if (ent) ent[P] = h;
+    if (sec) sec[P] = h2;
+}
+
 // ------------------------------------------------------------------------------ numpy sums
 // numpy float64 add.reduce (numpy 2.2, verified against np.add.reduce / np.mean in
 // test_summary_matches_numpy in tests/test_gpu_parity.py): the input is consumed in 8192-element buffers, s = 0; s += pw(buffer),
@@ -811,12 +877,29 @@ hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span) {
     return hipGetLastError();
 }
 
+// kernel 2 as k_stats_lane (one lane per position) instead of k_stats (one wave per column);
+// -DBC_STATS_LANE=0 builds the A/B variant
+#ifndef BC_STATS_LANE
+#define BC_STATS_LANE 1
+#endif
+constexpr bool kStatsLane = BC_STATS_LANE != 0;
+
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2, int32_t* cov,
                         double* pc, double* ent, double* sec, int32_t* scratch_counts_out) {
     if (L <= 0) return hipSuccess;
     int64_t blocks = (L + 63) / 64;  // one 64-position tile per block
     if (blocks > 256 * 8 * 8) blocks = 256 * 8 * 8;
     int32_t* h = const_cast<int32_t*>(hist);  // written only in scratch mode (scratch_counts_out)
+    if (kStatsLane) {
+        const unsigned lb = (unsigned)((L + 255) / 256);
+        if (k == 5)
+            hipLaunchKernelGGL(k_stats_lane<5>, dim3(lb), dim3(256), 0, s, h, L, nf, nf2, scratch_counts_out, cov, pc,
+                               ent, sec);
+        else
+            hipLaunchKernelGGL(k_stats_lane<6>, dim3(lb), dim3(256), 0, s, h, L, nf, nf2, scratch_counts_out, cov, pc,
+                               ent, sec);
+        return hipGetLastError();
+    }
     if (k == 5)
         hipLaunchKernelGGL(k_stats<5>, dim3((unsigned)blocks), dim3(64 * 5), 0, s, h, L, nf, nf2,
                            scratch_counts_out, cov, pc, ent, sec);

@@ -60,12 +60,21 @@ constexpr int kWaitVm0 = 0x0F70;
 #define BC_RC_EARLY_WAIT 1
 #endif
 constexpr bool kEarlyWait = BC_RC_EARLY_WAIT != 0;
-// chunk bounds without the index: reduced across the waves at the stage barrier (see `deferred`);
-// -DBC_RC_DEFER_BOUNDS=0 builds the A/B variant with its own block reduction barrier
+// chunk bounds without the index reduced across the waves at the stage barrier (see `deferred`):
+// measured slower (A/B, round 4: 44.2 vs 43.3 us single pass, and the indexed path 35.3 vs 33.4 us
+// from the larger kernel), so off; -DBC_RC_DEFER_BOUNDS=1 builds that variant
 #ifndef BC_RC_DEFER_BOUNDS
-#define BC_RC_DEFER_BOUNDS 1
+#define BC_RC_DEFER_BOUNDS 0
 #endif
 constexpr bool kDeferBounds = BC_RC_DEFER_BOUNDS != 0;
+// CIGAR words of the next chunk requested at the start of a chunk's image phase (fields kept two
+// chunks ahead) instead of after its expansion: measured slower on C3 (single-pass k_rc 44.2 vs
+// 43.2 µs over 3 A/B pairs: the longer-lived registers cost more than the earlier loads save), so
+// off; -DBC_RC_PF2=1 builds that variant
+#ifndef BC_RC_PF2
+#define BC_RC_PF2 0
+#endif
+constexpr bool kPf2 = BC_RC_PF2 != 0;
 #ifndef BC_RC_IGNORE_RECORDS
 #define BC_RC_IGNORE_RECORDS 0
 #endif
@@ -192,7 +201,8 @@ struct RcArgs {
     unsigned long long* err;
     int ablate;  // diagnostic only (BC_ABLATE): 4 no walk, 128 no folds, 256 trivial item events,
                  // 512 no staging, 2048 no flush, 8192 no event image, 16384 no image expansion,
-                 // 65536 no boundary rows in the image expansion
+                 // 65536 no boundary rows in the image expansion, 32768 no CIGAR load / decode,
+                 // 131072 decode a fixed CIGAR (no CIGAR words waited for), 262144 no CIGAR prefetch
     unsigned long long* trace;  // diagnostic only (BC_PHASE_TRACE builds): [block][wave][kRcPhases]
 };
 
@@ -330,22 +340,29 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     constexpr bool kRecordsOn = kRunsOn && !BC_RC_IGNORE_RECORDS;
     // the next chunk's per-read fields are loaded while the current one is walked
     uint32_t fpos = 0x7FFFFFFFu, fsn = 0, fcb = 0, fcn = 0, fsn_first = 0, fsn_last = 0;
-    auto fetch_fields = [&](IT ch) {
+    // kPf2 (CIGAR decode without the index): the fields one chunk further ahead (g*), so that the
+    // next chunk's CIGAR words can be requested as soon as a chunk's image phase begins
+    uint32_t gpos = 0x7FFFFFFFu, gsn = 0, gcb = 0, gcn = 0, gsn_first = 0, gsn_last = 0;
+    auto fetch_into = [&](IT ch, uint32_t& xpos, uint32_t& xsn, uint32_t& xcb, uint32_t& xcn, uint32_t& xfirst,
+                          uint32_t& xlast) {
         if (ch >= n_chunks) return;
         const IT b0 = ch * kRcReads;
         const int n = (int)(n_reads - b0 < kRcReads ? n_reads - b0 : kRcReads);
         if (tid < n) {
-            fpos = (uint32_t)*elem(A.pos, b0 + tid);
+            xpos = (uint32_t)*elem(A.pos, b0 + tid);
             if (!kRecordsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
-                fcb = *elem(A.cig_beg, b0 + tid);
-                fcn = *elem(A.cig_n, b0 + tid);
+                xcb = *elem(A.cig_beg, b0 + tid);
+                xcn = *elem(A.cig_n, b0 + tid);
             }
-            fsn = *elem(A.seq_nib, b0 + tid);
+            xsn = *elem(A.seq_nib, b0 + tid);
         }
-        fsn_first = sload(elem(A.seq_nib, b0));  // speculative staging bounds (reads usually lie in file order)
-        fsn_last = sload(elem(A.seq_nib, b0 + n - 1));
+        xfirst = sload(elem(A.seq_nib, b0));  // speculative staging bounds (reads usually lie in file order)
+        xlast = sload(elem(A.seq_nib, b0 + n - 1));
     };
+    auto fetch_fields = [&](IT ch) { fetch_into(ch, fpos, fsn, fcb, fcn, fsn_first, fsn_last); };
     fetch_fields((IT)blockIdx.x);
+    const bool pf2 = kPf2 && !(kRecordsOn && A.runs);  // (uniform)
+    if (pf2) fetch_into((IT)blockIdx.x + (IT)gridDim.x, gpos, gsn, gcb, gcn, gsn_first, gsn_last);
     // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
     // with qualities and six columns, which sit at the VGPR cap without it
     constexpr bool kPfOn = !(QUAL && NC == 6);
@@ -428,7 +445,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             if (valid) {
                 uint32_t w[kPre];
                 const bool use_pf = kPfOn && pf_ok && !runs && cmax <= kPf;  // (uniform)
-                if (use_pf) {
+                if (BC_ABL(A) & 131072) {  // diagnostic: decode a fixed 150M CIGAR (no loads waited for)
+#pragma unroll
+                    for (int i = 0; i < kPre; ++i) w[i] = i == 0 ? (150u << 4) : 0u;
+                } else if (use_pf) {
 #pragma unroll
                     for (int i = 0; i < kPre; ++i) w[i] = i < kPf ? pw[i] : 0u;
                 } else {
@@ -596,7 +616,26 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             __syncthreads();  // stage, records and the complex-read list complete
         }
         RC_STAMP(3);
-        if (kPfOn) fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
+        bool pf_early = false;
+        if (kPfOn && pf2) {
+            // the next chunk's fields arrived during this one (g*): its CIGAR words are requested
+            // now, a whole image phase earlier than below, and the fields of the chunk after it
+            // are fetched into g*
+            fpos = gpos, fsn = gsn, fcb = gcb, fcn = gcn, fsn_first = gsn_first, fsn_last = gsn_last;
+            fetch_into(chunk + 2 * (IT)gridDim.x, gpos, gsn, gcb, gcn, gsn_first, gsn_last);
+            if (chunk + (IT)gridDim.x < n_chunks) {
+                const IT nb0 = (chunk + (IT)gridDim.x) * kRcReads;
+                const int nn = (int)(n_reads - nb0 < kRcReads ? n_reads - nb0 : kRcReads);
+                const bool nv = tid < nn;
+                const int ncm = (BC_ABL(A) & 262144) ? 0 :  // diagnostic: no CIGAR prefetch
+                                    (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
+#pragma unroll
+                for (int i = 0; i < kPf; ++i) pw[i] = (nv && i < ncm && (uint32_t)i < fcn) ? A.cigar[fcb + i] : 0u;
+                pf_early = true;
+            }
+        } else if (kPfOn) {
+            fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
+        }
         if (img_path) {
             // ---- event image: thread tid writes column tid, rows = the chunk's windows
             // [G0, G0 + NWc): the 8 event classes its read has in each (zero outside the read)
@@ -733,10 +772,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 interior();
             }
         }
-        pf_ok = false;
+        pf_ok = pf_early;
         if (!kPfOn) {
             fetch_fields(chunk + (IT)gridDim.x);  // in flight during the walk
-        } else if (chunk + (IT)gridDim.x < n_chunks) {
+        } else if (!pf2 && chunk + (IT)gridDim.x < n_chunks) {
             const IT nb0 = (chunk + (IT)gridDim.x) * kRcReads;
             const int nn = (int)(n_reads - nb0 < kRcReads ? n_reads - nb0 : kRcReads);
             const bool nv = tid < nn;
@@ -746,7 +785,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     pw[0] = q.x, pw[1] = q.y, pw[2] = q.z, pw[3] = q.w;
                 }
             } else {
-                const int ncm = (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
+                const int ncm = (BC_ABL(A) & 262144) ? 0 :  // diagnostic: no CIGAR prefetch
+                                    (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
 #pragma unroll
                 for (int i = 0; i < kPf; ++i) pw[i] = (nv && i < ncm && (uint32_t)i < fcn) ? A.cigar[fcb + i] : 0u;
             }

@@ -1,9 +1,9 @@
 // bc_stats.h — kernel 2 for ONE position, evaluated by the position's lane: coverage,
 // percentages and the two entropies of main.py:29-53, in CPython's order of operations.
 //
-// Used where a kernel finalises positions one per lane (k_pileup_solo's tiles, k_rc's tiles
-// completed in-kernel).  k_stats spreads the same terms over one wave per column and adds them
-// in the same column order, so every path gives the same bits.
+// Used where a kernel finalises positions one per lane (k_pileup's and k_pileup_solo's tiles;
+// k_stats_lane restates it with a NULL check per output).  k_stats spreads the same terms over
+// one wave per column and adds them in the same column order, so every path gives the same bits.
 #pragma once
 #include <cstdint>
 

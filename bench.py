@@ -57,7 +57,7 @@ KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "solo": "k_pileup_sol
                 "rc_no_index": "k_rc without the device index (CIGAR words decoded in the kernel)",
                 "rc_indexed": "k_rc from a prebuilt device index (run records + chunk summaries of "
                               "k_index_runs, replayed; not the step)",
-                "stats": "k_stats (kernel 2)",
+                "stats": "k_stats_lane (kernel 2)",
                 "index": "k_index_runs + k_index_tiles (the batch's device index, bc_reads_index)",
                 "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)",
                 "solo_sum": "k_pileup_solo summary-only sweep (kernels 1 + 2 fused, numpy's partials, no per-position "
@@ -770,7 +770,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                     if dom == "pileup" else
                     "k_pileup_solo (sparse sweep, kernel 1 and kernel 2 fused), one launch per contig per step"
                     if dom == "solo" else
-                    "k_rc (kernel 1, into a zeroed scratch) + k_stats (kernel 2, moves the counts out "
+                    "k_rc (kernel 1, into a zeroed scratch) + k_stats_lane (kernel 2, moves the counts out "
                     "and re-zeroes) per contig per step")
                    + (", + numpy-exact summary per contig" if summarise else "")
                    + (", + RCCL gather of the summaries to rank 0" if gather is not None else "")

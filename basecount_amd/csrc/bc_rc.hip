@@ -75,6 +75,14 @@ constexpr bool kDeferBounds = BC_RC_DEFER_BOUNDS != 0;
 #define BC_RC_PF2 0
 #endif
 constexpr bool kPf2 = BC_RC_PF2 != 0;
+// reads per chunk chosen so that every resident block takes the same number of chunks (launch_rc):
+// measured slower (C3: 6 rounds of 218-read chunks 48.3 us against 5 rounds of 256 + a 67-chunk
+// tail 42.4 us; a round costs ~8.2 us whatever its reads, scripts/reads_sweep.sh), so off;
+// -DBC_RC_BALANCE=1 builds that variant
+#ifndef BC_RC_BALANCE
+#define BC_RC_BALANCE 0
+#endif
+constexpr bool kRcBalance = BC_RC_BALANCE != 0;
 #ifndef BC_RC_IGNORE_RECORDS
 #define BC_RC_IGNORE_RECORDS 0
 #endif
@@ -195,6 +203,7 @@ struct RcArgs {
     int64_t seq_words;
     int64_t qual_bytes;
     int64_t n_chunks;
+    int32_t chunk_reads;  // reads per chunk (<= the block's threads; the last chunk may hold fewer)
     const uint4* runs;  // bc_reads.read_runs (run records, bc_runs.h) or NULL: decode the CIGARs
     const uint4* sums;  // the upload's chunk summaries (2 x uint4 per chunk, after the records) or NULL
     int32_t* counts;  // [ncols][L], accumulated into
@@ -331,7 +340,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     uint8_t* stage = stage_raw + 4 * kPadW;
     auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     int64_t bad = INT64_MAX;
-    const IT n_reads = (IT)A.n, L = (IT)A.L, n_chunks = (IT)A.n_chunks;
+    const IT n_reads = (IT)A.n, L = (IT)A.L, n_chunks = (IT)A.n_chunks, CR = (IT)A.chunk_reads;
 
     // run records (bc_reads.read_runs) in place of the first decode: the variants with spare
     // registers (the others spill with the extra path)
@@ -346,8 +355,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     auto fetch_into = [&](IT ch, uint32_t& xpos, uint32_t& xsn, uint32_t& xcb, uint32_t& xcn, uint32_t& xfirst,
                           uint32_t& xlast) {
         if (ch >= n_chunks) return;
-        const IT b0 = ch * kRcReads;
-        const int n = (int)(n_reads - b0 < kRcReads ? n_reads - b0 : kRcReads);
+        const IT b0 = ch * CR;
+        const int n = (int)(n_reads - b0 < CR ? n_reads - b0 : CR);
         if (tid < n) {
             xpos = (uint32_t)*elem(A.pos, b0 + tid);
             if (!kRecordsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
@@ -400,8 +409,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
 #endif
     for (IT chunk = blockIdx.x; chunk < n_chunks; chunk += (IT)gridDim.x) {
         RC_STAMP(0);
-        const IT c0 = chunk * kRcReads;
-        const int nr = (int)(n_reads - c0 < kRcReads ? n_reads - c0 : kRcReads);
+        const IT c0 = chunk * CR;
+        const int nr = (int)(n_reads - c0 < CR ? n_reads - c0 : CR);
         // ---- 1. setup: one read per thread
         const bool valid = tid < nr;
         uint32_t mpos = 0x7FFFFFFFu, msn = 0, mcb = 0, mcn = 0;
@@ -624,8 +633,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             fpos = gpos, fsn = gsn, fcb = gcb, fcn = gcn, fsn_first = gsn_first, fsn_last = gsn_last;
             fetch_into(chunk + 2 * (IT)gridDim.x, gpos, gsn, gcb, gcn, gsn_first, gsn_last);
             if (chunk + (IT)gridDim.x < n_chunks) {
-                const IT nb0 = (chunk + (IT)gridDim.x) * kRcReads;
-                const int nn = (int)(n_reads - nb0 < kRcReads ? n_reads - nb0 : kRcReads);
+                const IT nb0 = (chunk + (IT)gridDim.x) * CR;
+                const int nn = (int)(n_reads - nb0 < CR ? n_reads - nb0 : CR);
                 const bool nv = tid < nn;
                 const int ncm = (BC_ABL(A) & 262144) ? 0 :  // diagnostic: no CIGAR prefetch
                                     (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
@@ -776,8 +785,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         if (!kPfOn) {
             fetch_fields(chunk + (IT)gridDim.x);  // in flight during the walk
         } else if (!pf2 && chunk + (IT)gridDim.x < n_chunks) {
-            const IT nb0 = (chunk + (IT)gridDim.x) * kRcReads;
-            const int nn = (int)(n_reads - nb0 < kRcReads ? n_reads - nb0 : kRcReads);
+            const IT nb0 = (chunk + (IT)gridDim.x) * CR;
+            const int nn = (int)(n_reads - nb0 < CR ? n_reads - nb0 : CR);
             const bool nv = tid < nn;
             if (runs) {  // (uniform) the next chunk's run records instead of its CIGAR words
                 if (nv) {
@@ -1097,9 +1106,21 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
 #endif
     constexpr int nt = kRcChunk;
     A.n_chunks = (r.n_reads + nt - 1) / nt;
+    A.chunk_reads = nt;
     A.sums = A.runs && r.run_chunks == A.n_chunks ? A.runs + r.n_reads : nullptr;
     // resident blocks: LDS bounds a CU to 3 (event image + stage + histogram)
     const int64_t cap = 256 * 3;
+    if (!A.sums && kRcBalance) {
+        // Every resident block takes the same number of chunks: the reads are cut into rounds x
+        // cap chunks of at most nt reads (rounds = what nt-read chunks need), instead of full
+        // chunks and a last round that only some blocks take (1M reads: 3,907 chunks = 5 rounds of
+        // 768 + 67, whose latency chain the whole launch waits for).  The upload's chunk summaries
+        // describe nt-read chunks, so the indexed path keeps them.
+        const int64_t rounds = (A.n_chunks + cap - 1) / cap;
+        const int64_t per = (r.n_reads + rounds * cap - 1) / (rounds * cap);
+        A.chunk_reads = (int32_t)(per < nt ? (per > 64 ? per : 64) : nt);  // (at least a wave of reads)
+        A.n_chunks = (r.n_reads + A.chunk_reads - 1) / A.chunk_reads;
+    }
     const int64_t blocks = A.n_chunks < cap ? A.n_chunks : cap;
     const dim3 grid((unsigned)blocks), block(nt);
     A.trace = nullptr;

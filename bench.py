@@ -270,7 +270,9 @@ class Workload:
             self.total_positions = sum(L for _, L in contigs)
         else:
             name = "MN908947.3" if world == 1 else f"contig{rank}"
-            self.rs = synth.make_reads([(name, c["contigs"][0][1])], c["reads"], c["mixed"],
+            # BC_BENCH_READS: diagnostic read-count override (experiments only; the line says so)
+            nreads = int(os.environ.get("BC_BENCH_READS") or c["reads"])
+            self.rs = synth.make_reads([(name, c["contigs"][0][1])], nreads, c["mixed"],
                                        c["seed"] + 1000 * rank)
             self.total_positions = world * self.rs.lengths[0]
         self.k = 5
@@ -770,6 +772,9 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                     if dom == "pileup" else
                     "k_pileup_solo (sparse sweep, kernel 1 and kernel 2 fused), one launch per contig per step"
                     if dom == "solo" else
+                    "k_pileup_solo summary-only sweep (kernels 1 + 2 fused, numpy's partials, no per-position "
+                    "output), one launch per contig per step"
+                    if dom == "solo_sum" else
                     "k_rc (kernel 1, into a zeroed scratch) + k_stats_lane (kernel 2, moves the counts out "
                     "and re-zeroes) per contig per step")
                    + (", + numpy-exact summary per contig" if summarise else "")
@@ -1231,7 +1236,8 @@ def main():
             "scaling": head["scaling"],
             "vs_baseline": None,
             "dtype": "int32 counts / f64 stats",
-            "data": "synthetic (seeded, BASELINE config shape)",
+            "data": "synthetic (seeded, BASELINE config shape)" + (
+                f"; DIAGNOSTIC read count {os.environ['BC_BENCH_READS']}" if os.environ.get("BC_BENCH_READS") else ""),
             "config": {"workload": head["workload"], "reads_per_rank": head["reads_per_rank"],
                        "positions_per_rank": head["positions_per_rank"],
                        "contigs_per_rank": head["contigs_per_rank"], "min_base_quality": args.mbq,

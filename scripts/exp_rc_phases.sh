@@ -13,7 +13,7 @@ cp scripts/tmp/lib_trace.so $LIB
 for m in idx noidx; do
   extra="--read-runs off"; [ $m = idx ] && extra="--read-runs on"
   BC_TRACE=gpurun_out/rc_$m.bin timeout -k 10 300 python bench.py --config c3 --no-extras --no-e2e --no-cpu-baseline \
-    --steps 20 --warmup 5 --launch eager --lean $extra > gpurun_out/tr_$m.log 2>&1
+    --steps 20 --warmup 5 --launch eager --lean --allow-diag $extra > gpurun_out/tr_$m.log 2>&1
   rc=$?; echo "trace $m rc=$rc"; [ $rc -eq 0 ] || { cp /tmp/lib_orig.so $LIB; tail -5 gpurun_out/tr_$m.log; exit $rc; }
   python scripts/trace_rc.py gpurun_out/rc_$m.bin
 done

@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} ;;
+    tests) run tests 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=25 ${PYTEST_ARGS} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS} ;;
     bench3) run bench3 600 python bench.py --config c3 --no-cpu-baseline --no-extras ${BENCH_ARGS} ;;
     bench5) run bench5 600 python bench.py --config c5 --no-cpu-baseline --no-extras --steps 10 --warmup 2 ${BENCH_ARGS} ;;

@@ -12,3 +12,7 @@ print(f"blocks {t.shape[0]}; per-wave total cycles median {np.median(tot):.0f}")
 for w in range(4):
     share = t[:, w, :].sum(axis=0) / t[:, w, :].sum()
     print(f"wave {w}: " + "  ".join(f"{n} {100 * s:.1f}%" for n, s in zip(names, share) if s > 0))
+# absolute: median per-wave cycles of each phase, summed over the wave's chunks
+med = np.median(t, axis=0)
+for w in range(4):
+    print(f"wave {w} cycles: " + "  ".join(f"{n} {m:.0f}" for n, m in zip(names, med[w]) if m > 0))

@@ -15,6 +15,28 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+def pytest_runtest_logstart(nodeid, location):
+    """On a gpurun box ($GRAFT_REPO_ROOT), the test being started is appended to
+    gpurun_out/progress.log: a long multi-rank test shows progress there, and a hung one is named."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if root:
+        import time
+
+        os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(root, "gpurun_out", "progress.log"), "a") as fh:
+            fh.write(f"{time.strftime('%H:%M:%S')} {nodeid}\n")
+
+
+def progress(msg: str) -> None:
+    """A line in gpurun_out/progress.log from inside a long test (no-op off the box)."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if root:
+        import time
+
+        with open(os.path.join(root, "gpurun_out", "progress.log"), "a") as fh:
+            fh.write(f"{time.strftime('%H:%M:%S')}   {msg}\n")
+
+
 @pytest.fixture(scope="session")
 def golden():
     return GOLDEN

@@ -7,6 +7,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -138,18 +139,34 @@ def test_bench_gpus_2_rehearsal():
 CONTIGS6 = [("c0", 30_000), ("c1", 5_000), ("c2", 80_000), ("c3", 12_000), ("c4", 50_000), ("c5", 9_000)]
 
 
-def _ranks(world, args, tmp_path, name, extra_env=None, cwd=None):
+def _ranks(world, args, tmp_path, name, extra_env=None, cwd=None, timeout=100):
     """Run the CLI on `world` ranks (gloo); (return codes, stdout bytes, stderr texts)."""
     out = tmp_path / f"{name}.out"
     env = dict(os.environ, PYTHONPATH=REPO, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
-               BASECOUNT_DIST_BACKEND="gloo", PYTHONHASHSEED="0", **(extra_env or {}))
+               BASECOUNT_DIST_BACKEND="gloo", PYTHONHASHSEED="0", BASECOUNT_HANG_DUMP=str(timeout - 20),
+               **(extra_env or {}))
+    from conftest import progress
+
+    progress(f"{world} rank(s): {' '.join(args[1:])} {extra_env or ''}")
     with open(out, "wb") as fh:
         procs = []
         for r in range(world):
             e = dict(env, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r)) if world > 1 else env
             procs.append(subprocess.Popen([sys.executable, "-m", "basecount_amd", *args], stdout=fh,
                                           stderr=subprocess.PIPE, env=e, cwd=cwd))
-        errs = [p.communicate(timeout=600)[1].decode() for p in procs]
+        # one deadline for all ranks; a rank still running then (a collective that never
+        # completes) fails the test with every rank's stderr, which holds its stack
+        # (BASECOUNT_HANG_DUMP) instead of hanging the session
+        deadline, errs = time.monotonic() + timeout, []
+        try:
+            for p in procs:
+                errs.append(p.communicate(timeout=max(1.0, deadline - time.monotonic()))[1].decode())
+        except subprocess.TimeoutExpired:
+            for p in procs:
+                p.kill()
+            errs = [p.communicate()[1].decode(errors="replace") for p in procs]
+            raise AssertionError(f"{world} ranks still running after {timeout} s: {args}\n" +
+                                 "\n".join(f"--- rank {r}\n{e[-6000:]}" for r, e in enumerate(errs)))
     return [p.returncode for p in procs], out.read_bytes(), errs
 
 

@@ -449,6 +449,14 @@ int bc_reads_sort(bc_ctx* c, const bc_reads* r, bc_reads* out, void* d_mem, size
     uint32_t overflow = 0;
     HIP_TRY(hipMemcpyAsync(&overflow, bc::sort_overflow_word(*r, d_mem), 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (overflow == 4u) {  // reads of very different lengths: the fixed relay slots do not fit
+        {
+            Timed tm(c, BC_K_SORT);
+            HIP_TRY(bc::launch_sort(c->stream, *r, tmp, d_mem, true));
+        }
+        HIP_TRY(hipMemcpyAsync(&overflow, bc::sort_overflow_word(*r, d_mem), 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     if (overflow & 2u) return fail(BC_E_ARG, "bc_reads_sort: a read starts outside [0, max_end] (max_end not truthful)");
     if (overflow) return fail(BC_E_ARG, "bc_reads_sort: the reads' sequences overlap (sorted copy would not fit)");
     *out = tmp;

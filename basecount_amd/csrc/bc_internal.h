@@ -103,9 +103,12 @@ inline bool pileup_is_solo(const bc_reads& r, int64_t L, int shape, int tile_wav
 
 // ---- the coordinate-sorted copy of an unsorted batch (bc_sort.hip) ----
 size_t sort_bytes(const bc_reads& r);
-// enqueues the sort into mem (sort_bytes(r) bytes) and fills `out` (sorted, no index)
-hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem);
-// device word set when the sorted sequence would not fit its buffer (read after a sync)
+// enqueues the sort into mem (sort_bytes(r) bytes) and fills `out` (sorted, no index): the relay
+// into fixed slots, or with `exact` the gather, scanned offsets and copy
+hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem, bool exact = false);
+// device word set when the sorted sequence would not fit its buffer (read after a sync): bit 0
+// the exact steps' sequences overlap, bit 1 a start outside [0, max_end], bit 2 the fixed
+// relay slots do not fit (run the exact steps)
 const uint32_t* sort_overflow_word(const bc_reads& r, void* mem);
 
 // ---- the device index of a sorted batch (bc_index.hip) ----

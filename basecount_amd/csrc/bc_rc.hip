@@ -83,6 +83,14 @@ constexpr bool kPf2 = BC_RC_PF2 != 0;
 #define BC_RC_BALANCE 0
 #endif
 constexpr bool kRcBalance = BC_RC_BALANCE != 0;
+// gather staging of chunks whose sequence is not one short segment (see `gather`); -DBC_RC_GATHER=0
+// builds the variant that walks such chunks from HBM
+#ifndef BC_RC_GATHER
+#define BC_RC_GATHER 1
+#endif
+constexpr bool kGather = BC_RC_GATHER != 0;
+constexpr int kRcSlot = 76;  // stage bytes per read in gather staging (152 nibbles: 150-bp reads at either parity)
+static_assert(kRcSlot % 4 == 0 && kRcSlot * kRcChunk <= 78 * kRcChunk, "gather slots fit the stage");
 #ifndef BC_RC_IGNORE_RECORDS
 #define BC_RC_IGNORE_RECORDS 0
 #endif
@@ -559,16 +567,26 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             decode(std::integral_constant<int, kMaxRuns>{});
         }
         seg_lo = seg_hi > seg_lo ? (seg_lo & ~15u) : 0u;
-        if (cx && !deferred) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         const bool spec_ok = spec && (seg_hi <= seg_lo || (seg_lo >= spec_lo && seg_hi <= spec_hi));
         if (spec_ok) seg_lo = spec_lo;  // the stage holds [spec_lo, spec_hi)
         const bool staged = spec_ok || seg_hi - seg_lo <= (uint32_t)kStage;
+        // Gather staging: the chunk's sequence is not one short segment (the reads of a batch
+        // sorted on the device without relaying its sequence, bc_sort.hip): every simple read's
+        // bytes are copied to its own kRcSlot-byte slot of the stage instead, and a read longer
+        // than its slot is walked as a complex read (rc_complex, from HBM).
+        const bool gather = kGather && !QUAL && !deferred && !staged && !sums && !(BC_ABL(A) & 512);  // (uniform)
+        const bool big = gather && simple && ((((msn & 1u) + T.qlen + 1u) >> 1) > (uint32_t)kRcSlot);
+        const bool cxa = cx || big, simplea = simple && !big;
+        const bool inlds = staged || gather;  // (uniform) the walks read the stage
+        // the read's first base as a nibble index of the stage (or of the batch's buffer)
+        const uint32_t rel = gather ? (uint32_t)(2 * kRcSlot * tid) + (msn & 1u) : msn - (staged ? 2u * seg_lo : 0u);
+        if (cxa && !deferred) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         // event-image path: a staged chunk of reads with <= 2 runs whose windows fit the image.
         // Each read's events are extracted ONCE per window (lane = read, its windows in a row)
         // instead of once per (window, run) item from the run table.
         const IT WBc = P0 & ~(IT)7;
         const int NWc = (int)(P1 > WBc ? (P1 - WBc + 7) / 8 : 0);
-        const bool img_path = staged && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
+        const bool img_path = inlds && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
         const int gpad = NWc;  // (uniform) the image's group padding (see rec)
         uint32_t* const mycol = img + tid * kImgRows + (tid >> 5) * gpad;  // this read's image column
         if (spec && !spec_ok && !deferred) {  // (uniform) the speculative copy is overwritten
@@ -604,17 +622,30 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 *(uint4*)(stage + off) = q4;
             }
         }
+        if (gather && simplea) {
+            // the read's bytes from its first base on, 4-byte words funnel-shifted from the aligned
+            // words around them (up to 7 bytes past the read: the buffer is padded), into its slot
+            const uint32_t from = msn >> 1, nw = ((((msn & 1u) + T.qlen + 1u) >> 1) + 3u) >> 2;
+            const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
+            const uint32_t sh = (from & 3u) * 8u;
+            uint32_t* d32 = (uint32_t*)(stage + kRcSlot * tid);
+            uint32_t wv[kRcSlot / 4 + 1];
+#pragma unroll
+            for (int w = 0; w <= kRcSlot / 4; ++w) wv[w] = (uint32_t)w <= nw ? s32[w] : 0u;
+#pragma unroll
+            for (int w = 0; w < kRcSlot / 4; ++w)
+                if ((uint32_t)w < nw) d32[w] = __builtin_amdgcn_alignbit(wv[w + 1], wv[w], sh);
+        }
         // ---- records (pos kept for complex / padding entries so pos[] stays sorted)
         {
-            const uint32_t qbase = staged ? 2u * seg_lo : 0u;
             uint32_t rr[kMaxRuns], nb[kMaxRuns];
 #pragma unroll
             for (int k = 0; k < kMaxRuns; ++k) {
-                rr[k] = simple ? pack_rr(T.st[k], T.en[k]) : 0u;
-                nb[k] = msn - qbase + (uint32_t)T.qd[k];
+                rr[k] = simplea ? pack_rr(T.st[k], T.en[k]) : 0u;
+                nb[k] = rel + (uint32_t)T.qd[k];
             }
             if (!img_path) {
-                rec[tid * 3] = make_uint4(mpos, simple ? T.span * 4u : 0u, rr[0], nb[0]);
+                rec[tid * 3] = make_uint4(mpos, simplea ? T.span * 4u : 0u, rr[0], nb[0]);
                 rec[tid * 3 + 1] = make_uint4(rr[1], nb[1], rr[2], nb[2]);
                 rec[tid * 3 + 2] = make_uint4(rr[3], nb[3], 0u, 0u);
             }
@@ -651,9 +682,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             const int p7 = (int)(mpos & 7u);
             const int G0 = (int)(U((uint32_t)P0) >> 3);
             const int i0 = (int)(mpos >> 3) - G0;  // the read's first window row
-            const int qb = (int)(staged ? 2u * seg_lo : 0u);
             // run k: stage nibble of stream position 0 (= window row i0, nibble 0)
-            const int s0 = (int)msn - qb + T.qd[0] - p7, s1 = (int)msn - qb + T.qd[1] - p7;
+            const int s0 = (int)rel + T.qd[0] - p7, s1 = (int)rel + T.qd[1] - p7;
             const int wb0 = s0 >> 3, wb1 = s1 >> 3;
             const uint32_t sh0 = (uint32_t)(s0 & 7) * 4u, sh1 = (uint32_t)(s1 & 7) * 4u;
             // Stream bits (4 per nibble) from the image's first row: the read is [Z, SP), its
@@ -772,7 +802,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     }
                 }
             };
-            if (!simple || (BC_ABL(A) & 16384)) {
+            if (!simplea || (BC_ABL(A) & 16384)) {
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) mycol[row] = 0u;
             } else if (8 * (IT)(G0 + kImgRows) > L) {  // (uniform) rows may reach past L
@@ -801,8 +831,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             }
             pf_ok = true;
         }
-        const SeqSrc src{staged ? (const uint32_t*)stage : (const uint32_t*)A.seq,
-                         staged ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
+        const SeqSrc src{inlds ? (const uint32_t*)stage : (const uint32_t*)A.seq,
+                         inlds ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
         const IT WB = P0 & ~(IT)7;
         const int G0w = (int)(WB >> 3);  // the image's first window (image path)
         const IT NW = P1 > WB ? (P1 - WB + 7) / 8 : 0;
@@ -998,16 +1028,16 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     if (BC_ABL(A) & 256) {
                         x = rec[rs * 3].x * 0x01010101u;
                     } else if (maxrun <= 1) {
-                        x = gap ? (staged ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
-                                          : window_events<1, true, false, QUAL>(src, rec, rs, gb))
-                                : (staged ? window_events<1, false, true, QUAL>(src, rec, rs, gb)
-                                          : window_events<1, false, false, QUAL>(src, rec, rs, gb));
+                        x = gap ? (inlds ? window_events<1, true, true, QUAL>(src, rec, rs, gb)
+                                         : window_events<1, true, false, QUAL>(src, rec, rs, gb))
+                                : (inlds ? window_events<1, false, true, QUAL>(src, rec, rs, gb)
+                                         : window_events<1, false, false, QUAL>(src, rec, rs, gb));
                     } else if (maxrun == 2) {
-                        x = staged ? window_events<2, true, true, QUAL>(src, rec, rs, gb)
-                                   : window_events<2, true, false, QUAL>(src, rec, rs, gb);
+                        x = inlds ? window_events<2, true, true, QUAL>(src, rec, rs, gb)
+                                  : window_events<2, true, false, QUAL>(src, rec, rs, gb);
                     } else {
-                        x = staged ? window_events<4, true, true, QUAL>(src, rec, rs, gb)
-                                   : window_events<4, true, false, QUAL>(src, rec, rs, gb);
+                        x = inlds ? window_events<4, true, true, QUAL>(src, rec, rs, gb)
+                                  : window_events<4, true, false, QUAL>(src, rec, rs, gb);
                     }
                     return rr < ghi ? x : 0u;
                 };

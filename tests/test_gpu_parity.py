@@ -71,6 +71,11 @@ def random_batch(rng, L, n, long_skip=False, sort=True, nfrac=0.05):
         quals.append(rng.integers(0, 45, q).astype(np.uint8))
         pos.append(int(rng.integers(0, L - span)))
         cigs.append(ops)
+    return build_batch(pos, cigs, seqs, quals, sort)
+
+
+def build_batch(pos, cigs, seqs, quals, sort=True):
+    """The batch dict of reads given as starts, CIGAR (op, len) lists, base codes and qualities."""
     order = np.argsort(pos, kind="stable") if sort else np.arange(len(pos))
     pos = [pos[i] for i in order]
     cigs = [cigs[i] for i in order]
@@ -330,15 +335,19 @@ def test_reads_index_on_device_slices(ctx, shape):
     whole.free()
 
 
-@pytest.mark.parametrize("seed,L,n,mbq", [(71, 3_000, 20_000, 0), (72, 30_000, 60_000, 20), (73, 500, 5, 0),
-                                          (74, 2_000_000, 3_000, 40), (75, 6_000, 40_000, 20)])
-def test_device_sort_of_unsorted_batch(ctx, seed, L, n, mbq):
-    """bc_reads_sort: an unsorted batch put in start order on the device (counting sort + the
-    sequence / quality relayout); the sorted copy's starts are non-decreasing, it keeps every
-    read, and every kernel shape on it gives the unsorted batch's counts (count.cpp's sums do
-    not depend on the order)."""
+@pytest.mark.parametrize("seed,L,n,mbq,qual", [(71, 3_000, 20_000, 0, True), (72, 30_000, 60_000, 20, True),
+                                               (73, 500, 5, 0, True), (74, 2_000_000, 3_000, 40, True),
+                                               (75, 6_000, 40_000, 20, True), (76, 3_000, 60_000, 0, False),
+                                               (77, 500, 3, 0, False)])
+def test_device_sort_of_unsorted_batch(ctx, seed, L, n, mbq, qual):
+    """bc_reads_sort: an unsorted batch put in start order on the device (radix sort of the
+    starts + the sequence / quality relay into fixed slots); the sorted copy's starts are
+    non-decreasing, it keeps every read, and every kernel shape on it gives the unsorted batch's
+    counts (count.cpp's sums do not depend on the order)."""
     rng = np.random.default_rng(seed)
     b = random_batch(rng, L, n, sort=False)
+    if not qual:
+        b = dict(b, qual=None)
     exp, (br, _) = O.bcount(L, mbq, b)
     assert br == -1
     r = D.DeviceReads(ctx, b)
@@ -364,6 +373,94 @@ def test_device_sort_of_unsorted_batch(ctx, seed, L, n, mbq):
             got = hist.download(np.int32, k * L).reshape(k, L)
             assert np.array_equal(got, exp[:, :k].T.astype(np.int32)), (shape, k)
     r.free()
+
+
+@pytest.mark.parametrize("mbq", [0, 30])
+def test_device_sort_exact_path_for_mixed_lengths(ctx, mbq):
+    """A batch of short reads and one 6,000-base read: the fast sort's fixed relay slots (the
+    longest read's bytes each) would not fit the copy's buffer, so bc_reads_sort runs the exact
+    path (counting sort + scanned offsets); same counts, sorted starts."""
+    rng = np.random.default_rng(91)
+    L, n = 20_000, 3_000
+    pos = [int(x) for x in rng.integers(0, L - 60, n)]
+    cigs = [[(0, 40)] for _ in range(n)]
+    pos.append(100)
+    cigs.append([(0, 3_000), (1, 3_000), (0, 10)])  # 6,010 query bases
+    seqs = [synth.ACGT[rng.integers(0, 4, sum(ln for op, ln in c if op in (0, 1, 4, 7, 8)))] for c in cigs]
+    quals = [rng.integers(0, 45, q.size).astype(np.uint8) for q in seqs]
+    b = build_batch(pos, cigs, seqs, quals, sort=False)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    r = D.DeviceReads(ctx, b)
+    nb = ctx.sort_bytes(r)
+    mem = ctx.alloc(nb)
+    s = ctx.sort(r, mem.ptr, nb)
+    got_pos = np.zeros(s.n_reads, np.int32)
+    D.check(D.lib().bc_memcpy_d2h(ctx.h, got_pos.ctypes.data, s.pos, got_pos.nbytes))
+    ctx.sync()
+    assert np.array_equal(got_pos, np.sort(b["pos"]))
+    for shape in ("auto", "rc"):
+        ctx.set_shape(shape)
+        hist = ctx.alloc(4 * 5 * L)
+        hist.zero()
+        ctx.count(s, L, mbq, 5, hist.ptr)
+        assert ctx.range_error() == -1
+        assert np.array_equal(hist.download(np.int32, 5 * L).reshape(5, L), exp[:, :5].T.astype(np.int32)), shape
+        hist.free()
+    ctx.set_shape("auto")
+    r.free()
+
+
+def scatter_sequences(b, rng):
+    """The batch with every read's sequence bytes moved to a random place of a new buffer (its
+    nibble parity and soft-clip offset kept): the same reads, no contiguous segment per chunk."""
+    cig = b["cigar"]
+    n = b["pos"].size
+    q = np.zeros(n, np.int64)
+    clip = np.zeros(n, np.int64)
+    for i in range(n):
+        ws = cig[b["cig_beg"][i]: b["cig_beg"][i] + b["cig_n"][i]]
+        ops, lens = ws & 15, ws >> 4
+        q[i] = int(lens[np.isin(ops, (0, 1, 4, 7, 8))].sum())
+        clip[i] = int(lens[0]) if ops.size and ops[0] == 4 else 0
+    start = (b["seq_nib"].astype(np.int64) - clip) // 2  # each read's first byte
+    nbytes = (q + 1) // 2
+    order = rng.permutation(n)
+    off = np.zeros(n, np.int64)
+    off[order] = np.concatenate([[0], np.cumsum(nbytes[order] + rng.integers(0, 3, n))[:-1]])
+    seq = np.zeros(int((off + nbytes).max()) + 8, np.uint8)
+    qual = np.zeros(2 * seq.size, np.uint8) if b.get("qual") is not None else None
+    for i in range(n):
+        seq[off[i]: off[i] + nbytes[i]] = b["seq"][start[i]: start[i] + nbytes[i]]
+        if qual is not None:
+            qual[2 * off[i]: 2 * (off[i] + nbytes[i])] = b["qual"][2 * start[i]: 2 * (start[i] + nbytes[i])]
+    return dict(b, seq=seq, qual=qual, seq_nib=(2 * off + clip).astype(np.uint32))
+
+
+@pytest.mark.parametrize("seed,L,n", [(81, 3_000, 40_000), (82, 30_000, 20_000), (83, 1_000, 300)])
+@pytest.mark.parametrize("mbq", [0, 20])
+def test_rc_gather_staging_of_scattered_sequence(ctx, seed, L, n, mbq):
+    """A sorted batch whose reads' sequences lie scattered in their buffer (not one segment per
+    chunk): k_rc copies each read's bytes into its own stage slot (gather staging; reads longer
+    than a slot are walked from HBM) and counts exactly what the oracle counts."""
+    rng = np.random.default_rng(seed)
+    b = scatter_sequences(random_batch(rng, L, n), rng)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    r = D.DeviceReads(ctx, b)
+    ctx.set_shape("rc")
+    try:
+        for k in (5, 6):
+            hist = ctx.alloc(4 * k * L)
+            hist.zero()
+            ctx.count(r, L, mbq, k, hist.ptr)
+            assert ctx.range_error() == -1
+            got = hist.download(np.int32, k * L).reshape(k, L)
+            assert np.array_equal(got, exp[:, :k].T.astype(np.int32)), k
+            hist.free()
+    finally:
+        ctx.set_shape("auto")
+        r.free()
 
 
 def test_rc_event_image_range_error(ctx):

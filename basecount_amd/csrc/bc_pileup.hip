@@ -767,6 +767,10 @@ __device__ __forceinline__ void advance_cursor(const int32_t* pos, IT n, IT& cur
 // main.py:469-499): no per-position output at all but the last partial buffer's coverage and
 // entropy; the summary partials alone are written, and a quarter buffer with no reads is one
 // constant store (its 16 leaves are 128.0 each: 2048.0, exactly).
+// per wave: a quarter's 16 leaves, then the 64-double transposition scratch (80 doubles: four
+// 4-wave workgroups with their records and stages fit a CU's 160 KiB of LDS)
+constexpr int kLeafDoubles = 16 + 64;
+static_assert(4 * (4 * (kRecBytes + kStageRegion) + 4 * kLeafDoubles * 8) <= 160 * 1024, "4 workgroups per CU");
 template <bool QUAL, int K, bool STATS, bool SUMP, typename IT, bool STORE = true>
 __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     static_assert(STORE || (STATS && SUMP), "the summary-only sweep computes the summary partials");
@@ -804,8 +808,8 @@ __global__ __launch_bounds__(256, 4) void k_pileup_solo(PileArgs A) {
     // kernel joins the 4 quarters of a buffer
     double e_prev = 0.0;
     bool prev_empty = false;
-    double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + 128 * wave;
-    double* mytr = myleaves + 64;  // transposition scratch of the leaf sums
+    double* myleaves = (double*)(dyn + (size_t)nw * (kRecBytes + kStageRegion)) + kLeafDoubles * wave;
+    double* mytr = myleaves + 16;  // transposition scratch of the leaf sums (64 doubles)
     long long sum_cov = 0, sum_nz = 0;
     // SUMP: tile t's share of numpy's pairwise leaves (h: its entropies; an empty tile's are 1.0)
     auto leaf_step = [&](IT t, bool empty, double h) {
@@ -1054,7 +1058,7 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
         int64_t blocks = (waves + nw - 1) / nw;
         blocks = (blocks + 7) / 8 * 8;  // a multiple of the XCD count (see the kernel's tile mapping)
         const dim3 grid((unsigned)blocks), block(64 * nw);
-        const size_t lds = (size_t)nw * (kRecBytes + kStageRegion) + (sump ? (size_t)nw * 128 * 8 : 0);
+        const size_t lds = (size_t)nw * (kRecBytes + kStageRegion) + (sump ? (size_t)nw * kLeafDoubles * 8 : 0);
         // 32-bit reads and positions when they fit (the cursor loop then stays on the scalar unit)
         const bool i32 = A.n < (int64_t)0x7FFFFF00 && A.n_tiles * kTile + A.max_span + 2 * kTile < (int64_t)0x7FFFFF00;
 #define BC_SOLO(Q, KK, ST)                                                                                       \

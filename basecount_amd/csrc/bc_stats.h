@@ -30,7 +30,16 @@ __device__ __forceinline__ double position_stats(const uint32_t* c, int64_t L, i
     }
     cov_out[P] = (int32_t)cov;
     double h = 1.0, h2 = 1.0;
-    if (cov != 0) {
+    if (cov != 0 && cov == (int64_t)mx) {
+        // one class only (most covered positions of a shallow batch): p = 1 for it and 0 for the
+        // rest, so the terms are exactly what the loops below would give: -(1 * log2 1) = -0.0,
+        // 0.0 + -0.0 = 0.0, h = nf * 0.0 = 0.0; pc 100.0 and 0.0; cov2 = 0 leaves h2 = 1.0
+        if (pc) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) pc[(int64_t)j * L + P] = j == am ? 100.0 : 0.0;
+        }
+        h = 0.0;
+    } else if (cov != 0) {
         double s = 0.0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
@@ -69,7 +78,12 @@ __device__ __forceinline__ double position_entropy(const uint32_t* c, double nf,
     for (int j = 0; j < K; ++j) cov += c[j];
     cov_out = (uint32_t)cov;
     double h = 1.0;
-    if (cov != 0) {
+    uint32_t mx = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) mx = c[j] > mx ? c[j] : mx;
+    if (cov != 0 && cov == (int64_t)mx) {
+        h = 0.0;  // one class only: -(1 * log2 1) = -0.0 summed from 0.0, times nf (as above)
+    } else if (cov != 0) {
         double s = 0.0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {

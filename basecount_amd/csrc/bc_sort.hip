@@ -209,12 +209,13 @@ __global__ __launch_bounds__(256) void k_sort_perm(SortArgs A) {
 // bytes of a relay slot: the largest read's aligned bases at either nibble parity, in words
 __device__ __forceinline__ uint32_t relay_slot(uint32_t qmax) { return ((qmax + 2u) / 2u + 3u) & ~3u; }
 
-// Sorted reads j, fast variant (4 lanes per read, kRelayReads reads per lane group with their
-// loads batched so each lane has many in flight): read i = perm[j]'s 32-byte record gathered, its
-// fields written, its sequence bytes copied word by word (two aligned source words and a funnel
-// shift; the source is read up to 3 bytes past the read, inside the padded buffer) into slot j,
-// its qualities into slot j of the quality copy; the new nibble index keeps the old one's parity.
-// Bytes of a slot past its read are never read.
+// Reads i in SOURCE order (4 lanes per read, kRelayReads consecutive reads per lane group, their
+// loads batched so each lane has many in flight): read i's 32-byte record (coalesced), its sorted
+// slot j = scanned bin of its start + its rank in the bin (no permutation array), its fields
+// written to slot j, its sequence bytes copied word by word (two aligned source words and a funnel
+// shift; the source is read up to 3 bytes past the read, inside the padded buffer: consecutive
+// reads' bytes are adjacent, so the loads stream) into slot j of the copy, its qualities likewise.
+// The new nibble index keeps the old one's parity.  Bytes of a slot past its read are never read.
 constexpr int kRelayReads = 4;
 constexpr int kRelayWords = 5;  // words per lane per read in the unrolled part (20 per read: 160 bases)
 __global__ __launch_bounds__(256) void k_sort_relay(SortArgs A) {
@@ -227,23 +228,29 @@ __global__ __launch_bounds__(256) void k_sort_relay(SortArgs A) {
         if (g == 0) atomicOr(A.overflow, 4u);
         return;
     }
-    uint32_t ii[kRelayReads];
-#pragma unroll
-    for (int r = 0; r < kRelayReads; ++r) ii[r] = A.perm[j0 + r < A.n ? j0 + r : j0];
     uint4 a[kRelayReads];
-    uint32_t q[kRelayReads];
+    uint32_t q[kRelayReads], jj[kRelayReads];
 #pragma unroll
     for (int r = 0; r < kRelayReads; ++r) {
-        a[r] = A.rec[2 * (size_t)ii[r]];  // {pos, cig_beg, cig_n, seq_nib}
-        q[r] = A.rec[2 * (size_t)ii[r] + 1].x;
+        const size_t i = (size_t)(j0 + r < A.n ? j0 + r : j0);  // source read
+        a[r] = A.rec[2 * i];  // {pos, cig_beg, cig_n, seq_nib}
+        const uint4 b = A.rec[2 * i + 1];  // {qlen, rank}
+        q[r] = b.x;
+        jj[r] = b.y;
     }
+#pragma unroll
+    for (int r = 0; r < kRelayReads; ++r) jj[r] += A.bins[a[r].x];  // the read's sorted slot
     {  // lane `sub` writes read j0 + sub's fields
         uint4 me = a[0];
 #pragma unroll
         for (int r = 1; r < kRelayReads; ++r)
             if (sub == (uint32_t)r) me = a[r];
-        const int64_t j = j0 + sub;
-        if (j < A.n) {
+        uint32_t mj = jj[0];
+#pragma unroll
+        for (int r = 1; r < kRelayReads; ++r)
+            if (sub == (uint32_t)r) mj = jj[r];
+        if (j0 + sub < A.n) {
+            const uint32_t j = mj;
             A.o_pos[j] = (int32_t)me.x;
             A.o_cig_beg[j] = me.y;
             A.o_cig_n[j] = me.z;
@@ -263,8 +270,8 @@ __global__ __launch_bounds__(256) void k_sort_relay(SortArgs A) {
     }
 #pragma unroll
     for (int r = 0; r < kRelayReads; ++r) {
-        const int64_t j = j0 + r;
-        if (j >= A.n) break;  // (uniform in the lane group)
+        if (j0 + r >= A.n) break;  // (uniform in the lane group)
+        const uint32_t j = jj[r];
         const uint32_t sn = a[r].w, from = sn >> 1, words = ((((sn & 1u) + q[r] + 1u) >> 1) + 3u) >> 2;
         const uint32_t sh = (from & 3u) * 8u;
         const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
@@ -438,7 +445,7 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     if (exact) hipLaunchKernelGGL(k_sort_count<false>, dim3(blocks), dim3(256), 0, s, A);
     else hipLaunchKernelGGL(k_sort_count<true>, dim3(blocks), dim3(256), 0, s, A);
     if ((e = scan_u32(s, A.bins, L.nbins, tmp, nullptr)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sort_perm, dim3(blocks), dim3(256), 0, s, A);
+    if (exact) hipLaunchKernelGGL(k_sort_perm, dim3(blocks), dim3(256), 0, s, A);
     if (!exact) {
         const int64_t groups = (r.n_reads + kRelayReads - 1) / kRelayReads;
         hipLaunchKernelGGL(k_sort_relay, dim3((unsigned)((groups * 4 + 255) / 256)), dim3(256), 0, s, A);

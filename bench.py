@@ -368,28 +368,34 @@ class Workload:
             ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
                              [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
 
-    def pipelined(self, steps: int, side):
-        """K steps with two in flight: they alternate between the main context and ``side`` (each
-        with its own read-chunked scratch and output buffers), so a step's kernel 2 and the next
-        step's kernel 1 overlap, as consecutive batches of a stream would.  Enqueued (and
-        capturable) on the main context: fork, two chains of steps, join."""
+    def pipelined(self, steps: int, sides: list):
+        """K steps with 1 + len(sides) in flight: step i runs on context i mod n (the main one or
+        a side context, each with its own read-chunked scratch and output buffers), so a step's
+        kernel 2 and tail overlap the next steps' kernel 1, as consecutive batches of a stream
+        would.  Enqueued (and capturable) on the main context: fork, n chains of steps, join."""
         main = self.ctx
+        ctxs = [main] + list(sides)
         if not hasattr(self, "_pipe_out"):
-            k = self.k
-            self._pipe_out = []
-            for _, L, _, _, o in self.work:
-                self._pipe_out.append(dict(counts=main.alloc(4 * k * L), cov=main.alloc(4 * L),
-                                           pc=main.alloc(8 * k * L) if self.want_pc else None,
-                                           ent=main.alloc(8 * L), sec=main.alloc(8 * L)))
-        side.wait(main)
+            self._pipe_out = {}
+        k = self.k
+        for n in range(1, len(ctxs)):  # output buffers of side context n (context 0: the step's own)
+            if n not in self._pipe_out:
+                self._pipe_out[n] = [dict(counts=main.alloc(4 * k * L), cov=main.alloc(4 * L),
+                                          pc=main.alloc(8 * k * L) if self.want_pc else None,
+                                          ent=main.alloc(8 * L), sec=main.alloc(8 * L))
+                                     for _, L, _, _, _ in self.work]
+        for side in sides:
+            side.wait(main)
         for i in range(steps):
-            c = main if i % 2 == 0 else side
+            n = i % len(ctxs)
+            c = ctxs[n]
             j = self._next()
-            for (_, L, _, reads, o), o2 in zip(self.work, self._pipe_out):
-                out = o if i % 2 == 0 else o2
+            for w, (_, L, _, reads, o) in enumerate(self.work):
+                out = o if n == 0 else self._pipe_out[n][w]
                 c.pileup(reads[j], L, self.mbq, self.k, self.nf, self.nf2, out["counts"].ptr, out["cov"].ptr,
                          out["pc"].ptr if out["pc"] is not None else None, out["ent"].ptr, out["sec"].ptr)
-        main.wait(side)
+        for side in sides:
+            main.wait(side)
 
     def variant(self, name: str):
         """Per copy and contig, a bc_reads of the same device batch: "no_index" without its
@@ -509,11 +515,12 @@ class Workload:
             for v in o.values():
                 if v is not None:
                     v.free()
-        for o in getattr(self, "_pipe_out", []):
-            for v in o.values():
-                if v is not None:
-                    v.free()
-        self._pipe_out = []
+        for outs in getattr(self, "_pipe_out", {}).values():
+            for o in outs:
+                for v in o.values():
+                    if v is not None:
+                        v.free()
+        self._pipe_out = {}
         if self.d_sum is not None:
             self.d_sum.free()
         self.work = []
@@ -563,54 +570,64 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         if gather is not None:
             gather_step()
 
-    # Consecutive steps are independent batches: with --pipeline 2 (the default for the one-stream
-    # configs) the K timed steps run two in flight, alternating between two contexts (own scratch
-    # and outputs; fork / join inside the one captured graph), so a step's tail overlaps the next
-    # step's head as a stream of batches runs.  Every step still does all of its work; the
+    # Consecutive steps are independent batches: with --pipeline P (P > 1, the one-stream configs)
+    # the K timed steps may run up to P in flight, step i on context i mod n (own scratch and
+    # outputs; fork / join inside the one captured graph), so a step's tail overlaps the next
+    # steps' heads as a stream of batches runs.  Every step still does all of its work; the
     # serialized step time is reported beside it (serial_us_per_step).
-    pipe = (args.pipeline == 2 and launch == "graph" and gather is None and not summarise
+    pipe = (args.pipeline > 1 and launch == "graph" and gather is None and not summarise
             and len(wl.ctxs) == 1 and not args.lean)
-    side = None
+    sides = []
     if pipe:
         from basecount_amd import device as Dm
 
-        side = Dm.Context(ctx.device)
-        side.set_shape(args.shape, args.tile_waves)
+        for _ in range(args.pipeline - 1):
+            sides.append(Dm.Context(ctx.device))
+            sides[-1].set_shape(args.shape, args.tile_waves)
     for _ in range(warmup):
         step()
     if pipe:
-        wl.pipelined(max(2, warmup), side)  # (also allocates the side context's scratch, uncaptured)
-        side.sync()
+        # (also allocates the side contexts' scratch and outputs, uncaptured)
+        wl.pipelined(max(len(sides) + 1, warmup), sides)
+        for sd in sides:
+            sd.sync()
     ctx.sync()
-    if ctx.range_error() != -1 or (side is not None and side.range_error() != -1):
+    if ctx.range_error() != -1 or any(sd.range_error() != -1 for sd in sides):
         raise RuntimeError(f"{cfg}: out-of-range event in a synthetic batch")
     graph = None
     trial = None
+    in_flight = 1
     if launch == "graph" and gather is None:  # the same K steps, replayed from one captured graph
-        graph = ctx.capture((lambda: wl.pipelined(steps, side)) if pipe else (lambda: [step() for _ in range(steps)]))
-        graph.launch()  # untimed replay (first-launch setup)
-        ctx.sync()
         if pipe:
-            # Two steps in flight pay a fixed cost per graph launch (the two-stream graph's fork /
-            # join and its nodes' cross-stream dependencies: ~60 us), which a short run
-            # does not amortise.  Both K-step graphs are replayed untimed, alternately, and the
-            # timed region launches the faster one for this K (`launch_trial` in the line).
-            serial_g = ctx.capture(lambda: [step() for _ in range(steps)])
-            serial_g.launch()
+            # n steps in flight pay a fixed cost per graph launch (the n-stream graph's fork / join
+            # and its nodes' cross-stream dependencies: ~60 us at n = 2), which a short
+            # run does not amortise, and past some n the steps only contend.  The K-step graphs for
+            # n = 1 .. P are replayed untimed, alternately, and the timed region launches the
+            # fastest for this K (`launch_trial` in the line).
+            graphs = {1: ctx.capture(lambda: [step() for _ in range(steps)])}
+            for n in range(2, len(sides) + 2):
+                graphs[n] = ctx.capture(lambda n=n: wl.pipelined(steps, sides[:n - 1]))
+            for g in graphs.values():
+                g.launch()  # untimed replay (first-launch setup)
             ctx.sync()
-            best = {"two_in_flight": float("inf"), "serial": float("inf")}
+            # (wall clock around launch + sync, as the timed region measures `value`: a graph of
+            # more streams costs more to submit, which device events would not see)
+            best = {n: float("inf") for n in graphs}
             for _ in range(3):
-                for name, g in (("two_in_flight", graph), ("serial", serial_g)):
-                    ctx.event_record(2)
-                    g.launch()
-                    ctx.event_record(3)
+                for n, g in graphs.items():
                     ctx.sync()
-                    best[name] = min(best[name], ctx.event_elapsed_ms(2, 3) * 1e3 / steps)
-            trial = {k: round(v, 3) for k, v in best.items()}
-            if best["serial"] < best["two_in_flight"]:
-                graph, pipe = serial_g, False
-            else:
-                del serial_g
+                    t1 = time.perf_counter()
+                    g.launch()
+                    ctx.sync()
+                    best[n] = min(best[n], (time.perf_counter() - t1) * 1e6 / steps)
+            trial = {("serial" if n == 1 else f"{n}_in_flight"): round(v, 3) for n, v in best.items()}
+            in_flight = min(best, key=best.get)
+            graph = graphs[in_flight]  # (the others are released after the timed region)
+            pipe = in_flight > 1
+        else:
+            graph = ctx.capture(lambda: [step() for _ in range(steps)])
+            graph.launch()  # untimed replay (first-launch setup)
+            ctx.sync()
     if group is not None:
         group.barrier()
     ctx.sync()
@@ -628,6 +645,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     elapsed = max_over_ranks(group, time.perf_counter() - t0)
     dev_step = ctx.event_elapsed_ms(0, 1) * 1e-3 / steps
     del graph
+    if trial is not None:
+        del graphs
 
     # which kernels a step launches (library timing facility, per-launch event pairs)
     ctx.timing(True)
@@ -708,20 +727,24 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
             extra_us["raw_step_us"] = extra_us["index_step_us"]
         del g
     if trial is not None:
-        # the same K steps serialized on one stream, one graph: the step's own latency
+        # the same K steps serialized on one stream, one graph: the step's own latency, on the
+        # timed region's basis (wall clock around the launch and sync) and in device time
         g = ctx.capture(lambda: [step() for _ in range(steps)])
         g.launch()
         ctx.sync()
+        t1 = time.perf_counter()
         ctx.event_record(2)
         g.launch()
         ctx.event_record(3)
-        extra_us["serial_us_per_step"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        ctx.sync()
+        extra_us["serial_us_per_step"] = (time.perf_counter() - t1) * 1e6 / steps
+        extra_us["serial_device_us_per_step"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
         if wl.single_pass and "rc" in launched:  # a whole step from the raw batch, serialized
-            extra_us["raw_step_us"] = extra_us["serial_us_per_step"]
+            extra_us["raw_step_us"] = extra_us["serial_device_us_per_step"]
         del g
-    if side is not None:
-        side.sync()
-        side.close()
+    for sd in sides:
+        sd.sync()
+        sd.close()
     gather_us = None
     if gather is not None:
         if group is not None:
@@ -781,12 +804,14 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                    + (", + RCCL gather of the summaries to rank 0" if gather is not None else "")
                    + (", the K timed steps replayed from one hipGraph" if launch == "graph" and gather is None
                       else ", eager launches")
-                   + (", two steps in flight (two streams, alternating)" if pipe else ""),
-        "steps_in_flight": 2 if pipe else 1,
+                   + (f", {in_flight} steps in flight ({in_flight} streams, step i on stream i mod {in_flight})"
+                      if pipe else ""),
+        "steps_in_flight": in_flight,
         "launch_trial": (None if trial is None else
-                         {"device_us_per_step": trial, "chosen": "two_in_flight" if pipe else "serial",
-                          "what": "both K-step graphs replayed untimed 3x each before the timed region; the "
-                                  "faster one is timed"}),
+                         {"us_per_step": trial, "basis": "wall clock around each graph's launch and sync",
+                          "chosen": f"{in_flight}_in_flight" if pipe else "serial",
+                          "what": "the K-step graphs with 1 (serial) to --pipeline steps in flight replayed "
+                                  "untimed 3x each before the timed region; the fastest one is timed"}),
         "reads_per_rank": int(sum(int(w[2]["pos"].size) for w in wl.work)),
         "positions_per_rank": int(sum(w[1] for w in wl.work)),
         "contigs_per_rank": len(wl.work),
@@ -1095,9 +1120,9 @@ def main():
     ap.add_argument("--read-runs", choices=["on", "off"], default="off",
                     help="on: the read-chunked step takes the upload's device index (run records + chunk "
                          "summaries); off (default): the single pass from the raw CIGAR words")
-    ap.add_argument("--pipeline", type=int, choices=[1, 2], default=2,
-                    help="steps in flight in the timed graph (2: consecutive batches overlap on two "
-                         "streams; 1: serialized)")
+    ap.add_argument("--pipeline", type=int, choices=[1, 2, 3, 4], default=4,
+                    help="most steps in flight in the timed graph (consecutive batches overlap on up to "
+                         "that many streams; the launch trial picks the fastest count; 1: serialized)")
     ap.add_argument("--rotate", type=int, default=0,
                     help="device copies of each batch the steps rotate over (0: 3 for c3, whose 110 MB "
                          "would otherwise stay in the 256 MB Infinity Cache, else 1)")
@@ -1276,6 +1301,7 @@ def main():
         line["launch_trial"] = head.get("launch_trial")
         if "serial_us_per_step" in head:
             line["serial_us_per_step"] = head["serial_us_per_step"]
+            line["serial_device_us_per_step"] = head.get("serial_device_us_per_step")
         if cpu:
             line["speedup_vs_cpu"] = head["value"] / cpu["value"]
             line["speedup_vs_cpu_all_cores"] = head["value"] / cpu_all["value"]

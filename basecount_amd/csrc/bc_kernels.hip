@@ -404,6 +404,88 @@ __global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, 
     if (sec) sec[P] = h2;
 }
 
+// Kernel 2 with eight lanes per position: lane j < K computes column j's percentage and its two
+// entropy terms (one division and log2 each: dependent fp64 chains K times shorter than
+// k_stats_lane's, over 8x the lanes), then the position's first lane adds the terms in column
+// order, as position_stats does.  Every lane holds all K counts (K in-group shuffles), so cov,
+// the maximum and np.argmax come from the same code as in position_stats; the results are those
+// of k_stats / k_stats_lane bit for bit.  NULL cov / pc / ent / sec are skipped as there.
+template <int K>
+__global__ __launch_bounds__(256) void k_stats_oct(int32_t* __restrict__ hist, int64_t L, double nf, double nf2,
+                                                   int32_t* __restrict__ counts_out, int32_t* __restrict__ cov_out,
+                                                   double* __restrict__ pc, double* __restrict__ ent,
+                                                   double* __restrict__ sec) {
+    __shared__ __attribute__((aligned(16))) double tab[64][4];
+    const int j = threadIdx.x & 7;
+    const int64_t P = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+    const bool in = P < L, col = in && j < K;
+    const uint32_t cj = col ? (uint32_t)hist[(int64_t)j * L + P] : 0u;
+    if (threadIdx.x < 128)
+        *(double2*)&tab[threadIdx.x >> 1][2 * (threadIdx.x & 1)] =
+            *(const double2*)&log2d::kTab[threadIdx.x >> 1][2 * (threadIdx.x & 1)];
+    __syncthreads();
+    if (col && counts_out) {
+        counts_out[(int64_t)j * L + P] = (int32_t)cj;
+        hist[(int64_t)j * L + P] = 0;
+    }
+    uint32_t c[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) c[i] = (uint32_t)__shfl((int)cj, i, 8);
+    int64_t cov = 0;
+    int am = 0;
+    uint32_t mx = c[0];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        cov += c[i];
+        if (c[i] > mx) mx = c[i], am = i;  // np.argmax: first maximum
+    }
+    const bool one = cov != 0 && cov == (int64_t)mx;  // one class only: the terms are exact constants
+    const int64_t cov2 = cov - (int64_t)mx;
+    double t = 0.0, u = 0.0;
+    if (col && cov != 0) {
+        if (one) {
+            if (pc) pc[(int64_t)j * L + P] = j == am ? 100.0 : 0.0;
+        } else {
+            const double pj = (double)cj / (double)cov;
+            if (pc) pc[(int64_t)j * L + P] = 100.0 * pj;
+            if (cj != 0) t = -(pj * glibc_log2_t(pj, tab));
+            if (sec && cov2 != 0 && j != am && cj != 0) {
+                const double q = (double)cj / (double)cov2;
+                u = -(q * glibc_log2_t(q, tab));
+            }
+        }
+    } else if (col && pc) {
+        pc[(int64_t)j * L + P] = -1.0;
+    }
+    double ts[K], us[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        ts[i] = __shfl(t, i, 8);
+        us[i] = __shfl(u, i, 8);
+    }
+    if (!in || j != 0) return;
+    if (cov_out) cov_out[P] = (int32_t)cov;
+    double h = 1.0, h2 = 1.0;
+    if (one) {
+        h = 0.0;
+    } else if (cov != 0) {
+        double s1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (c[i] != 0) s1 = s1 + ts[i];
+        h = nf * s1;
+        if (cov2 != 0) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i != am && c[i] != 0) s2 = s2 + us[i];
+            h2 = nf2 * s2;
+        }
+    }
+    if (ent) ent[P] = h;
+    if (sec) sec[P] = h2;
+}
+
 // ------------------------------------------------------------------------------ numpy sums
 // numpy float64 add.reduce (numpy 2.2, verified against np.add.reduce / np.mean in
 // test_summary_matches_numpy in tests/test_gpu_parity.py): the input is consumed in 8192-element buffers, s = 0; s += pw(buffer),
@@ -877,12 +959,13 @@ hipError_t launch_span(hipStream_t s, const bc_reads& r, int* d_max_span) {
     return hipGetLastError();
 }
 
-// kernel 2 as k_stats_lane (one lane per position) instead of k_stats (one wave per column);
-// -DBC_STATS_LANE=0 builds the A/B variant
+// kernel 2's shape: 1 = k_stats_lane (one lane per position), 2 = k_stats_oct (eight lanes per
+// position: 6.8 vs 7.1 us per launch by event pairs, but the C3 step 37.2-38.3 vs 36.5-37.1 us,
+// A/B x2), 0 = k_stats (one wave per column); -DBC_STATS_LANE=<n> builds the A/B variants
 #ifndef BC_STATS_LANE
 #define BC_STATS_LANE 1
 #endif
-constexpr bool kStatsLane = BC_STATS_LANE != 0;
+constexpr int kStatsShape = BC_STATS_LANE;
 
 hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, double nf, double nf2, int32_t* cov,
                         double* pc, double* ent, double* sec, int32_t* scratch_counts_out) {
@@ -890,7 +973,17 @@ hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, do
     int64_t blocks = (L + 63) / 64;  // one 64-position tile per block
     if (blocks > 256 * 8 * 8) blocks = 256 * 8 * 8;
     int32_t* h = const_cast<int32_t*>(hist);  // written only in scratch mode (scratch_counts_out)
-    if (kStatsLane) {
+    if (kStatsShape == 2) {
+        const unsigned ob = (unsigned)((L + 31) / 32);
+        if (k == 5)
+            hipLaunchKernelGGL(k_stats_oct<5>, dim3(ob), dim3(256), 0, s, h, L, nf, nf2, scratch_counts_out, cov, pc,
+                               ent, sec);
+        else
+            hipLaunchKernelGGL(k_stats_oct<6>, dim3(ob), dim3(256), 0, s, h, L, nf, nf2, scratch_counts_out, cov, pc,
+                               ent, sec);
+        return hipGetLastError();
+    }
+    if (kStatsShape == 1) {
         const unsigned lb = (unsigned)((L + 255) / 256);
         if (k == 5)
             hipLaunchKernelGGL(k_stats_lane<5>, dim3(lb), dim3(256), 0, s, h, L, nf, nf2, scratch_counts_out, cov, pc,

@@ -5,16 +5,17 @@
 // and its HBM traffic dominate.  Here a 256-thread block takes 256 CONSECUTIVE reads of the
 // sorted batch (a chunk), so each read is loaded, CIGAR-decoded and staged exactly once:
 //
-//   1. thread i: read c0 + i -> run table (bc_walk.h) -> 48 B record in LDS; the chunk's packed
-//      sequence (BC_SEQ_EVENT, bases below min_base_quality cleared) is staged into LDS;
-//   2. the chunk covers reference positions [P0, P1); they are cut into 8-position windows and
-//      the (window, 64-read slice) work items are split contiguously over the 4 waves, so a wave
-//      changes window only a few times per chunk (its counter folds stay wave-uniform);
-//   3. lane = read of the slice: the window's 8 event classes are one funnel shift per run, the
-//      six columns are SWAR nibble counters; a fold sums the 8 lanes of a group with DPP and adds
-//      the totals into an LDS histogram of the chunk's positions (16-bit column pairs);
-//   4. the LDS histogram is flushed into the int32 counts with coalesced global atomics (a
-//      position receives one add per chunk overlapping it).
+//   1. thread i: read c0 + i -> its CIGAR's first two runs (decode_fast2, or the upload's run
+//      records) ; the chunk's packed sequence (BC_SEQ_EVENT, bases below min_base_quality
+//      cleared) is staged into LDS (one segment by LDS-DMA, or per-read slots: gather staging);
+//   2. event image (chunks of reads with <= 2 runs): thread i writes its read's 8-position window
+//      words into column i of an LDS image [read][row]; the transposed sum counts each row's 32
+//      reads bit-sliced (carry-save trees + an 8x8 bit transpose) into per-position class counts;
+//      other chunks walk run tables: (window, 64-read slice) items over the 4 waves, SWAR nibble
+//      counters folded by DPP into an LDS histogram;
+//   3. the chunk's counts are flushed into the int32 counts with coalesced global atomics (a
+//      position receives one add per chunk overlapping it), an image chunk's by wave 3 during
+//      the next chunk's sum.
 //
 // Reads with more than 8 CIGAR ops / 4 runs / huge spans are walked separately with global
 // atomics.  Counted events at positions >= L are the reference's std::out_of_range

@@ -92,6 +92,13 @@ constexpr bool kRcBalance = BC_RC_BALANCE != 0;
 constexpr bool kGather = BC_RC_GATHER != 0;
 constexpr int kRcSlot = 76;  // stage bytes per read in gather staging (152 nibbles: 150-bp reads at either parity)
 static_assert(kRcSlot % 4 == 0 && kRcSlot * kRcChunk <= 78 * kRcChunk, "gather slots fit the stage");
+// the next chunk's fields requested at the chunk's start (behind its stage copy) instead of after
+// the stage barrier: no measurable change (C3 single pass 45.5-46.1 vs 45.8-45.9 us, A/B x3), so
+// off; -DBC_RC_FIELDS_EARLY=1 builds that variant
+#ifndef BC_RC_FIELDS_EARLY
+#define BC_RC_FIELDS_EARLY 0
+#endif
+constexpr bool kFieldsEarly = BC_RC_FIELDS_EARLY != 0;
 #ifndef BC_RC_IGNORE_RECORDS
 #define BC_RC_IGNORE_RECORDS 0
 #endif
@@ -444,6 +451,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // the copy's round trip).  They were issued a whole phase ago: this wait is ~free.
         if (kEarlyWait) __builtin_amdgcn_s_waitcnt(kWaitVm0);
         if (spec) stage_dma<kRcThreads>(stage, A.seq + spec_lo, spec_hi - spec_lo, tid);
+        // (kFieldsEarly) the next chunk's fields requested behind the stage copy, so they have
+        // arrived when its CIGAR words are prefetched after the stage barrier
+        const bool fields_early = kFieldsEarly && kPfOn && !kPf2 && !(kRecordsOn && A.runs);  // (uniform)
+        if (fields_early) fetch_fields(chunk + (IT)gridDim.x);
         RunTable T;
         T.nrun = 0;
         T.gap = T.complex = false;
@@ -675,7 +686,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 pf_early = true;
             }
         } else if (kPfOn) {
-            fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
+            if (!fields_early) fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
         }
         if (img_path) {
             // ---- event image: thread tid writes column tid, rows = the chunk's windows

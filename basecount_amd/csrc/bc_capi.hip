@@ -228,6 +228,7 @@ int bc_ctx_destroy(bc_ctx* c) {
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->rc_scratch) (void)hipFree(c->rc_scratch);
     if (c->out_scratch) (void)hipFree(c->out_scratch);
+    if (c->sum_scratch) (void)hipFree(c->sum_scratch);
     if (c->h_err) (void)hipHostFree(c->h_err);
     for (auto& v : c->ev)
         for (auto& pr : v) {
@@ -584,12 +585,32 @@ int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, in
             parts.no_store = true;
             parts.ent_tail = (double*)c->out_scratch;
             parts.cov_tail = (int32_t*)((double*)c->out_scratch + bc::kNpBuf);
+#ifdef BC_SUM_SWEEP  // A/B builds only: the per-tile sweep k_pileup_solo<STORE = false>
             {
-                Timed tm(c, bc::pileup_is_solo(*r, L, c->shape, c->tile_waves) ? BC_K_SOLO : BC_K_PILEUP);
+                Timed tm(c, BC_K_SOLO);
                 HIP_TRY(bc::launch_pileup_tiles(c->stream, *r, L, r->max_end, mbq, k, true, false, nf, nf2, nullptr,
                                                 nullptr, nullptr, nullptr, nullptr, c->d_err, c->shape, c->tile_waves,
                                                 &parts));
             }
+#else
+            {
+                const size_t need = bc::sum_sparse_bytes(L);
+                if (need > c->sum_scratch_bytes) {  // grow-only, zeroed once (the kernels leave it zeroed)
+                    if (c->sum_scratch) {
+                        HIP_TRY(hipStreamSynchronize(c->stream));
+                        HIP_TRY(hipFree(c->sum_scratch));
+                        c->sum_scratch = nullptr;
+                        c->sum_scratch_bytes = 0;
+                    }
+                    HIP_TRY(hipMalloc(&c->sum_scratch, need));
+                    c->sum_scratch_bytes = need;
+                    HIP_TRY(hipMemsetAsync(c->sum_scratch, 0, need, c->stream));
+                }
+                Timed tm(c, BC_K_SOLO);
+                HIP_TRY(bc::launch_sum_sparse(c->stream, *r, L, mbq, k, nf, c->d_err, parts, c->sum_scratch,
+                                                 c->sum_scratch_bytes));
+            }
+#endif
             if (!parts.fused) return fail(BC_E_ARG, "internal: summary-only sweep without fused partials");
             // the fold's last partial buffer reads positions [full_chunks * 8192, L): the tail
             // arrays stand at that offset (only those elements are addressed)

@@ -25,6 +25,8 @@ struct bc_ctx {
     size_t rc_scratch_bytes = 0;
     void* out_scratch = nullptr;           // bc_pileup_partials without outputs: their stand-ins
     size_t out_scratch_bytes = 0;
+    void* sum_scratch = nullptr;           // the read-parallel summary's leaf arrays, kept zeroed
+    size_t sum_scratch_bytes = 0;
     // kernel-shape overrides (bc_ctx_set_shape); 0 = chosen from the batch
     int shape = BC_SHAPE_AUTO;
     int tile_waves = 0;
@@ -88,6 +90,13 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
                                bool stats, bool accumulate, double nf, double nf2, int32_t* counts, int32_t* cov,
                                double* pc, double* ent, double* sec, unsigned long long* d_err, int shape = 0,
                                int tile_waves = 0, SumParts* parts = nullptr);
+// Summary only (main.py:469-499) for a sparse sorted batch: the read-parallel summary (counted
+// positions per 128-position leaf, exact walks of the leaves two reads share, numpy's tree per
+// quarter) into parts' quarter partials and tail arrays; `scratch` (>= sum_sparse_bytes(L) bytes,
+// laid out by its capacity) zeroed when allocated, left zeroed.  Needs L >= kNpBuf.
+size_t sum_sparse_bytes(int64_t L);
+hipError_t launch_sum_sparse(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, int k, double nf,
+                             unsigned long long* d_err, SumParts& parts, void* scratch, size_t scratch_bytes);
 hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, int ncols, int32_t* counts,
                      unsigned long long* d_err);
 // bc_pileup / bc_count choose the read-chunked k_rc over the tiled k_pileup when a tile would

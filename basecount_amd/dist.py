@@ -108,8 +108,17 @@ def _rdzv_timeout() -> float:
 
 class CommInitError(RuntimeError):
     """The job's communicator could not be created on every rank.  Raised on EVERY rank (the ranks
-    vote, see rendezvous_init), so a caller that falls back (bench.py: gloo) does so on all ranks
-    alike and no rank is left waiting in a collective the others never join."""
+    vote, see rendezvous_init) after every init call has returned and the communicators that did
+    come up were destroyed, so a caller that falls back (bench.py: gloo) does so on all ranks alike,
+    with no library state left behind, and no rank is left waiting in a collective the others never
+    join."""
+
+
+class CommInitAbandoned(RuntimeError):
+    """Some rank's init call was still blocked in the library (ncclCommInitRank) when the ranks
+    voted.  Its thread is abandoned there and may hold runtime locks, so no rank may carry on in
+    this process, on any backend: raised on EVERY rank instead of CommInitError, and the caller
+    must end the process (bench.py: os._exit, non-zero)."""
 
 
 def _init_timeout() -> float:
@@ -118,37 +127,53 @@ def _init_timeout() -> float:
 
 
 def _run_with_timeout(fn, arg, timeout: float):
-    """fn(arg) in a daemon thread: (True, result) or (False, reason).  A call still blocked at the
-    timeout (a collective init whose peers never arrive) is abandoned with its thread."""
+    """fn(arg) in a daemon thread: ("ok", result), ("fail", reason) or ("hang", reason).  A call
+    still blocked at the timeout (a collective init whose peers never arrive) is abandoned with its
+    thread: the process must not go on (CommInitAbandoned)."""
     import threading
 
     box = {}
 
     def target():
         try:
-            box["v"] = (True, fn(arg))
+            box["v"] = ("ok", fn(arg))
         except Exception as e:  # noqa: BLE001 - reported to the other ranks, re-raised by the caller
-            box["v"] = (False, f"{type(e).__name__}: {e}")
+            box["v"] = ("fail", f"{type(e).__name__}: {e}")
 
     t = threading.Thread(target=target, daemon=True)
     t.start()
     t.join(timeout)
-    return box.get("v", (False, f"no result within {timeout:.0f} s (BASECOUNT_COMM_INIT_TIMEOUT)"))
+    return box.get("v", ("hang", f"no result within {timeout:.0f} s (BASECOUNT_COMM_INIT_TIMEOUT)"))
+
+
+_STATES = ("ok", "fail", "hang")
+
+
+def _send_msg(conn, state: str, text: str) -> None:
+    b = text.encode()
+    conn.sendall(struct.pack("<II", _STATES.index(state), len(b)) + b)
+
+
+def _recv_msg(conn) -> tuple:
+    code, n = struct.unpack("<II", _recv_exact(conn, 8))
+    return _STATES[code] if code < len(_STATES) else "fail", _recv_exact(conn, n).decode(errors="replace")
 
 
 def rendezvous_init(rank: int, world: int, make_id, init, timeout: float | None = None,
-                    init_timeout: float | None = None):
+                    init_timeout: float | None = None, destroy=None):
     """A communicator created by agreement of all ranks, over one TCP connection per peer to rank
     0 (port ``BASECOUNT_RDZV_PORT``, default MASTER_PORT + 1):
 
       1. rank 0 binds the port (failing at once, with the port in the message, if it is taken),
-         calls make_id() and sends its bytes to every peer (an empty id if make_id failed: every
-         rank then raises at once instead of waiting);
+         calls make_id(), waits until every peer has connected and only then sends the id's
+         bytes to all of them (an empty id if make_id failed: every rank then raises at once), so
+         no rank starts its init clock before the last one has arrived;
       2. every rank calls init(id) (the collective bc_comm_init) in a thread bounded by
          ``init_timeout`` (``BASECOUNT_COMM_INIT_TIMEOUT``, default 120 s);
-      3. every rank reports success or failure to rank 0, which answers all of them with the
-         verdict.  Unless every rank succeeded, every rank raises CommInitError, naming the
-         ranks that failed.
+      3. every rank reports ok / failed / still blocked to rank 0, which answers all of them
+         with the verdict.  Unless every rank succeeded, the ranks whose init succeeded call
+         destroy(result), and then every rank raises: CommInitAbandoned if some init was still
+         blocked (no rank may go on in the process), CommInitError otherwise (a fallback is safe).
 
     The peers retry the connection for ``timeout`` seconds (``BASECOUNT_RDZV_TIMEOUT``, default
     120).  Returns init's result."""
@@ -158,9 +183,21 @@ def rendezvous_init(rank: int, world: int, make_id, init, timeout: float | None 
     init_timeout = _init_timeout() if init_timeout is None else float(init_timeout)
     deadline = time.monotonic() + timeout
 
-    def verdict_of(statuses: list):
-        bad = [f"rank {r}: {w}" for r, (o, w) in enumerate(statuses) if not o]
-        return not bad, "; ".join(bad)
+    def verdict_of(statuses: list) -> tuple:
+        bad = [f"rank {r}: {w}" for r, (st, w) in enumerate(statuses) if st != "ok"]
+        state = ("hang" if any(st == "hang" for st, _ in statuses) else
+                 "fail" if bad else "ok")
+        return state, "; ".join(bad)
+
+    def conclude(state: str, why: str, mine: tuple):
+        if state == "ok":
+            return mine[1]
+        if mine[0] == "ok" and destroy is not None:  # no communicator is left behind
+            with contextlib.suppress(Exception):
+                destroy(mine[1])
+        if state == "hang":
+            raise CommInitAbandoned(f"communicator init still blocked on some rank ({why}): ending the process")
+        raise CommInitError(f"communicator not created on every rank: {why}")
 
     if rank == 0:
         srv = None
@@ -189,33 +226,31 @@ def rendezvous_init(rank: int, world: int, make_id, init, timeout: float | None 
                                         f"rendezvous at {addr}:{port} within {timeout:.0f} s") from e
                 conn.settimeout(init_timeout + timeout)
                 peer = struct.unpack("<I", _recv_exact(conn, 4))[0]
-                conn.sendall(struct.pack("<I", len(uid)) + uid)
                 conns.append((peer, conn))
+            for _, conn in conns:  # every peer is here: the id goes out to all of them together
+                conn.sendall(struct.pack("<I", len(uid)) + uid)
             if id_err is not None:
                 raise CommInitError(f"rank 0 could not create the communicator id: {id_err}") from id_err
-            ok, res = _run_with_timeout(init, uid, init_timeout)
-            statuses = [(ok, res if not ok else "")] + [(False, "no report")] * (world - 1)
+            mine = _run_with_timeout(init, uid, init_timeout)
+            statuses = [(mine[0], mine[1] if mine[0] != "ok" else "")] + [("fail", "no report")] * (world - 1)
             for peer, conn in conns:
                 try:
-                    n = struct.unpack("<I", _recv_exact(conn, 4))[0]
-                    msg = _recv_exact(conn, n).decode(errors="replace")
+                    st, msg = _recv_msg(conn)
                     if 0 < peer < world:
-                        statuses[peer] = (msg == "", msg)
+                        statuses[peer] = (st, msg)
                 except (OSError, ConnectionError) as e:
                     if 0 < peer < world:
-                        statuses[peer] = (False, f"lost ({e})")
-            good, why = verdict_of(statuses)
+                        statuses[peer] = ("fail", f"lost ({e})")
+            state, why = verdict_of(statuses)
             for _, conn in conns:
                 with contextlib.suppress(OSError):
-                    conn.sendall(struct.pack("<I", len(why.encode())) + why.encode())
+                    _send_msg(conn, state, why)
         finally:
             for _, conn in conns:
                 conn.close()
             if srv is not None:
                 srv.close()
-        if not good:
-            raise CommInitError(f"communicator not created on every rank: {why}")
-        return res
+        return conclude(state, why, mine)
     while True:
         try:
             s = socket.create_connection((addr, port), timeout=10)
@@ -235,17 +270,14 @@ def rendezvous_init(rank: int, world: int, make_id, init, timeout: float | None 
             raise CommInitError(f"rank {rank}: the rendezvous with rank 0 failed ({e})") from e
         if not uid:
             raise CommInitError(f"rank {rank}: rank 0 could not create the communicator id")
-        ok, res = _run_with_timeout(init, uid, init_timeout)
-        msg = b"" if ok else (res or "failed").encode()
+        mine = _run_with_timeout(init, uid, init_timeout)
         try:
-            s.sendall(struct.pack("<I", len(msg)) + msg)
-            (n,) = struct.unpack("<I", _recv_exact(s, 4))
-            why = _recv_exact(s, n).decode(errors="replace")
+            _send_msg(s, mine[0], "" if mine[0] == "ok" else (mine[1] or "failed"))
+            state, why = _recv_msg(s)
         except (OSError, ConnectionError) as e:
-            raise CommInitError(f"rank {rank}: no verdict from rank 0 ({e})") from e
-    if why:
-        raise CommInitError(f"communicator not created on every rank: {why}")
-    return res
+            # no verdict: rank 0 is gone.  An init still blocked here forbids going on.
+            state, why = ("hang" if mine[0] == "hang" else "fail"), f"rank {rank}: no verdict from rank 0 ({e})"
+    return conclude(state, why, mine)
 
 
 class RcclGroup(_GroupOps):
@@ -281,7 +313,8 @@ class RcclGroup(_GroupOps):
         # TSV output (the first collective runs inside the redirect too).  The ranks agree on the
         # outcome (rendezvous_init): either every rank has the communicator or every rank raises.
         with _stdout_to_stderr():
-            self.h = rendezvous_init(rank, world, make_id, init)
+            self.h = rendezvous_init(rank, world, make_id, init,
+                                     destroy=lambda h: L.bc_comm_destroy(C.c_void_p(h)))
             self.barrier()
 
     def barrier(self):

@@ -1185,7 +1185,13 @@ def run(argv=None):
                                     provided_once=True))
     from . import dist
 
-    group = dist.Group() if dist.env()[0] > 1 else None  # RCCL (default) or gloo, DESIGN.md §6
+    try:
+        group = dist.Group() if dist.env()[0] > 1 else None  # RCCL (default) or gloo, DESIGN.md §6
+    except dist.CommInitAbandoned as e:
+        # an init thread is still blocked inside RCCL on some rank: nothing may run after it in
+        # this process (not even interpreter shutdown's library teardown), on any rank
+        print(f"basecount: {e}", file=sys.stderr, flush=True)
+        os._exit(3)
     timing = os.environ.get("BASECOUNT_HIP_TIMING") not in (None, "", "0")
     t0 = None
     if timing:  # per-kernel device times and the wall time on stderr; stdout unchanged

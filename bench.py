@@ -49,15 +49,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 WORKLOADS = {
     "c2": "C2: 1 contig 29,903 bp, 100,000 reads x 150 bp, all-M CIGAR (per rank)",
     "c3": "C3: 1 contig 29,903 bp, 1,000,000 reads x 150 bp, mixed M/I/D/=/X/S CIGAR (per rank)",
+    "c4": "C4: C3's contig and reads (29,903 bp, 1,000,000 mixed-CIGAR reads) with the 98-amplicon ARTIC "
+          "BED, --summarise-with-bed: kernel 1 + 2, the numpy-exact summary and the amplicon vectors",
     "c5": "C5: 24 contigs with GRCh38 chr1-22,X,Y lengths (3.09 Gb), 50,000 reads x 150 bp each, "
           "all-M CIGAR; contigs sharded over the ranks, summary + RCCL gather to rank 0 per step",
 }
 KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "solo": "k_pileup_solo (sparse sweep, fused kernel 1 + 2)",
                 "rc": "k_rc (read-chunked kernel 1)",
                 "rc_no_index": "k_rc without the device index (CIGAR words decoded in the kernel)",
+                "pileup_no_index": "k_pileup without the tile index (each tile group searches pos[])",
                 "rc_indexed": "k_rc from a prebuilt device index (run records + chunk summaries of "
                               "k_index_runs, replayed; not the step)",
                 "stats": "k_stats_lane (kernel 2)",
+                "amplicons": "k_amplicon (per amplicon window: integer mean and radix-select median of the "
+                             "coverage, numpy mean and median of both entropies)",
                 "index": "k_index_runs + k_index_tiles (the batch's device index, bc_reads_index)",
                 "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)",
                 "solo_sum": "k_pileup_solo summary-only sweep (kernels 1 + 2 fused, numpy's partials, no per-position "
@@ -83,7 +88,15 @@ def kernel_bytes(kernel: str, rb: int, L: int, k: int, with_pc: bool = True) -> 
     # partial buffer's coverage + entropy (12 B per position)
     sum_only = rb + 24 * (L // 2048) + 12 * (L % 8192)
     return {"pileup": rb + 4 * k * L + stats_out, "solo": rb + 4 * k * L + stats_out, "rc": rb + 4 * k * L,
-            "rc_no_index": rb + 4 * k * L, "rc_indexed": rb + 4 * k * L, "stats": 4 * k * L + stats_out, "solo_sum": sum_only}[kernel]
+            "rc_no_index": rb + 4 * k * L, "rc_indexed": rb + 4 * k * L,
+            "pileup_no_index": rb + 4 * k * L + stats_out, "stats": 4 * k * L + stats_out, "solo_sum": sum_only}[kernel]
+
+
+def amplicon_bytes(tiles, L: int) -> int:
+    """Algorithmic bytes of one k_amplicon launch: every window's coverage (4 B), entropy and
+    secondary entropy (8 B each) read once, its bounds (16 B) and 6 doubles out per window."""
+    span = sum(max(0, min(b, L - 1) - max(a, 0) + 1) for a, b in tiles)
+    return 20 * span + (16 + 48) * len(tiles)
 
 
 def lib_sha16() -> str:
@@ -176,6 +189,40 @@ def cpu_baseline(rs, b, L: int, budget_s: float = 10.0, mbq: int = 0, what: str 
     return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind, "host": host_info(),
             "sample": f"{desc}; full {what} workload ({n} reads, {L} positions, min_base_quality {mbq}) x "
                       f"{done} runs, {dt * 1e3:.1f} ms per run, BAM decode excluded"}
+
+
+def cpu_baseline_c4(b, L: int, args, budget_s: float = 5.0) -> dict:
+    """C4 as the reference computes it (main.py:469-551 after count.bcount + get_stats): its
+    compiled count.cpp, get_stats' rows, then the summary and the amplicon loops (every tile
+    scans every position, np.mean / np.median per window), restated in oracle.summary_amplicons_py.
+    One core; the arguments are built once, untimed."""
+    import oracle as O
+    from basecount_amd import synth
+    from basecount_amd.scheme import load_scheme
+
+    with tempfile.NamedTemporaryFile("w", suffix=".bed", delete=False) as fh:
+        fh.write(synth.artic_bed())
+    try:
+        tiles = [(w["inside_start"], w["inside_end"]) for _, _, w in load_scheme(fh.name)]
+    finally:
+        os.remove(fh.name)
+    ref = O.ref_bcount()
+    n = int(b["pos"].size)
+    if ref is not None and args is not None:
+        def run():
+            rows = O.get_stats_py(ref(L, 0, *args), "ref")
+            O.summary_amplicons_py(rows, tiles)
+        kind, desc = "reference", "reference count.cpp (pybind11 bcount) + get_stats + main.py:469-551 summary and amplicon loops"
+    else:
+        def run():
+            rows = O.get_stats_py(O.bcount(L, 0, b)[0].tolist(), "ref")
+            O.summary_amplicons_py(rows, tiles)
+        kind, desc = "port", "oracle C restatement of bcount + get_stats + main.py:469-551 summary and amplicon loops"
+    dt, done = _loop(run, budget_s)
+    return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind, "host": host_info(),
+            "sample": f"{desc} (Python, restated in oracle.summary_amplicons_py); full C4 workload ({n} reads, "
+                      f"{L} positions, {len(tiles)} amplicon windows) x {done} runs, {dt * 1e3:.1f} ms per run, "
+                      "BAM decode excluded"}
 
 
 def cpu_baseline_all_cores(b, L: int, budget_s: float = 5.0) -> dict:
@@ -276,7 +323,19 @@ class Workload:
                                        c["seed"] + 1000 * rank)
             self.total_positions = world * self.rs.lengths[0]
         self.k = 5
-        self.want_pc = not self.per_contig  # c5 is only ever summarised: no percentages
+        # --summarise-with-bed (C4): the amplicon windows of the ARTIC BED (scheme.load_scheme)
+        self.tiles = None
+        if c.get("bed"):
+            from basecount_amd.scheme import load_scheme
+
+            with tempfile.NamedTemporaryFile("w", suffix=".bed", delete=False) as fh:
+                fh.write(synth.artic_bed())
+            try:
+                self.tiles = [(w["inside_start"], w["inside_end"]) for _, _, w in load_scheme(fh.name)]
+            finally:
+                os.remove(fh.name)
+        # summarised configs (c4, c5) never print percentages
+        self.want_pc = not self.per_contig and self.tiles is None
         self.summarise = summarise
         self.fused_summary = fused_summary
         # --summarise's step (main.py:469-499 prints six numbers per contig): no per-position output
@@ -323,6 +382,12 @@ class Workload:
             self.work.append((t, L, b, reads, bufs))
         # every contig's 4 summary doubles, contiguous: the rank's gather payload
         self.d_sum = ctx.alloc(32 * max(1, len(self.work))) if summarise else None
+        self.d_tiles = None
+        if self.tiles is not None:
+            lo = np.ascontiguousarray([a for a, _ in self.tiles], np.int64)
+            hi = np.ascontiguousarray([b for _, b in self.tiles], np.int64)
+            self.d_tiles = (ctx.alloc(lo.nbytes).upload(lo), ctx.alloc(hi.nbytes).upload(hi),
+                            ctx.alloc(48 * len(self.tiles)))
         # contigs are independent: with streams > 1 they run on several contexts' streams at once
         # (bc_ctx_wait fork / join around them), so one launch's tail overlaps the next launches;
         # contigs go to the streams longest first, each to the least loaded one (LPT)
@@ -367,6 +432,10 @@ class Workload:
         if self.summarise and self.fused_summary:  # every contig's fold, side by side
             ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
                              [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
+        if self.d_tiles is not None:  # the amplicon vectors (main.py:501-551) of the one contig
+            (_, L, _, _, o), (d_lo, d_hi, d_amp) = self.work[0], self.d_tiles
+            ctx.amplicons(o["cov"].ptr, o["ent"].ptr, o["sec"].ptr, L, d_lo.ptr, d_hi.ptr, len(self.tiles),
+                          d_amp.ptr)
 
     def pipelined(self, steps: int, sides: list):
         """K steps with 1 + len(sides) in flight: step i runs on context i mod n (the main one or
@@ -435,6 +504,14 @@ class Workload:
             self.ctx.pileup(per[j][0], L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
                             o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
 
+    def pileup_with(self, variant: str):
+        """The step's pileup on a variant of the batch (see variant())."""
+        j = self._next()
+        for i, (_, L, _, _, o) in enumerate(self.work):
+            r = self.variant(variant)[i][j][0]
+            self.ctx.pileup(r, L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr, o["cov"].ptr,
+                            o["pc"].ptr if o["pc"] is not None else None, o["ent"].ptr, o["sec"].ptr)
+
     def count_only(self, variant: str | None = None):
         j = self._next()
         for i, (_, L, _, reads, o) in enumerate(self.work):
@@ -455,6 +532,18 @@ class Workload:
 
         ok = True
         small = min(self.work, key=lambda w: w[1])
+        if self.tiles is not None:
+            # the step's printed numbers (main.py:469-551): the summary against numpy and every
+            # amplicon mean / median against the oracle's, over the oracle's per-position arrays
+            (t, L, b, _, o) = self.work[0]
+            exp, (bad, _) = O.bcount(L, self.mbq, b, nthreads=cpu_threads())
+            ocov, _, oent, osec = O.stats(exp, False, nthreads=cpu_threads())
+            s = self.d_sum.download(np.float64, 4)
+            ok = bad == -1 and s[0] == np.mean(ocov.astype(np.int64)) and s[1] == np.mean(oent)
+            ok = ok and int(s[2]) == int(np.count_nonzero(ocov))
+            amp = self.d_tiles[2].download(np.float64, 6 * len(self.tiles)).reshape(-1, 6)
+            want = np.asarray(O.amplicons(ocov, oent, osec, self.tiles), np.float64)
+            return bool(ok and np.array_equal(amp, want))
         if self.summary_only:
             # no per-position output: the four summary numbers (main.py:469-499), against numpy
             # over the oracle's coverage / entropies on the smallest contig, and the exact
@@ -523,6 +612,9 @@ class Workload:
         self._pipe_out = {}
         if self.d_sum is not None:
             self.d_sum.free()
+        for x in self.d_tiles or ():
+            x.free()
+        self.d_tiles = None
         self.work = []
 
 
@@ -548,7 +640,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
     max over ranks) and describe them."""
     from basecount_amd import device as D
 
-    copies = args.rotate if args.rotate > 0 else (3 if cfg == "c3" else 1)
+    copies = args.rotate if args.rotate > 0 else (3 if cfg in ("c3", "c4") else 1)
     wl = Workload(ctx, cfg, rank, world, args.mbq, summarise, args.summary_path == "fused",
                   args.tile_index == "on", args.streams if summarise else 1, args.read_runs == "on", copies,
                   summary_only)
@@ -678,7 +770,7 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
             for name, (n_launch, mean_us) in c.timing_report().items():
                 rep[name] = rep.get(name, 0.0) + n_launch * mean_us
             c.timing(False)
-        for name in ("pileup", "solo", "rc", "stats", "summary"):
+        for name in ("pileup", "solo", "rc", "stats", "summary", "amplicons"):
             if name in rep:
                 key = "solo_sum" if (name == "solo" and wl.summary_only) else name
                 kern_s[key] = rep[name] * 1e-6 / reps_t
@@ -704,6 +796,33 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         kern_s["stats"] = rep["stats"][1] * 1e-6
         if "index" in rep:
             kern_s["index"] = rep["index"][1] * 1e-6
+    if "pileup" in launched and not summarise and not args.lean:
+        # C2 from a raw batch: k_pileup searching pos[] with no tile index,
+        # the tile index build alone (k_index_tiles, per-launch events over many launches), and
+        # whole steps index build + k_pileup, K of them in one graph (serialized, device time)
+        kern_s["pileup_no_index"] = region(lambda: wl.pileup_with("no_index"), reps)
+        ctx.timing(True)
+        for _ in range(reps):
+            wl.rebuild()
+        rep = ctx.timing_report()
+        ctx.timing(False)
+        if "index" in rep:
+            kern_s["index"] = rep["index"][1] * 1e-6
+        g = ctx.capture(lambda: [wl.raw_step() for _ in range(steps)])
+        g.launch()
+        ctx.sync()
+        ctx.event_record(2)
+        g.launch()
+        ctx.event_record(3)
+        extra_us["raw_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        g = ctx.capture(lambda: [wl.pileup_with("no_index") for _ in range(steps)])
+        g.launch()
+        ctx.sync()
+        ctx.event_record(2)
+        g.launch()
+        ctx.event_record(3)
+        extra_us["no_index_step_us"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
+        del g
     if "rc" in launched and not summarise and not args.lean:
         if wl.single_pass:
             # the step decodes the CIGARs in k_rc (single pass); beside it, k_rc replaying a device
@@ -741,6 +860,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
         extra_us["serial_device_us_per_step"] = ctx.event_elapsed_ms(2, 3) * 1e3 / steps
         if wl.single_pass and "rc" in launched:  # a whole step from the raw batch, serialized
             extra_us["raw_step_us"] = extra_us["serial_device_us_per_step"]
+        if "pileup" in launched and "raw_step_us" in extra_us:
+            extra_us["indexed_step_us"] = extra_us["serial_device_us_per_step"]
         del g
     for sd in sides:
         sd.sync()
@@ -829,6 +950,19 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                      "algorithmic_bytes": kbytes},
     }
     res.update(extra_us)
+    if wl.tiles is not None and "amplicons" in kern_s:
+        ab = amplicon_bytes(wl.tiles, wl.work[0][1])
+        res["amplicon_roofline"] = {
+            "bound": "hbm", "achieved": ab / kern_s["amplicons"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ab / kern_s["amplicons"] / 1e9 / HBM_PEAK_GBS, "traffic": None,
+            "kernel": KERNEL_NAMES["amplicons"], "time_basis": "kernel's average duration (per-launch events)",
+            "algorithmic_bytes": ab, "windows": len(wl.tiles)}
+    if "pileup_no_index" in kern_s:
+        res["pileup_frac_without_index"] = (wl.bytes_dominant("pileup") / kern_s["pileup_no_index"] / 1e9
+                                            / HBM_PEAK_GBS)
+        res["index_us"] = kern_s.get("index", 0.0) * 1e6
+        res["step_input"] = ("the upload's tile index (k_index_tiles, untimed) + k_pileup; raw_step_us = index "
+                             "build + k_pileup from the raw batch, no_index_step_us = k_pileup searching pos[]")
     if "rc_no_index" in kern_s or "rc_indexed" in kern_s:
         nb = wl.bytes_dominant("rc")
         single = kern_s["rc"] if wl.single_pass else kern_s["rc_no_index"]
@@ -1161,13 +1295,18 @@ def main():
     ctx.set_shape(args.shape, args.tile_waves)
     group = None
     if world > 1:
-        from basecount_amd.dist import CommInitError, Group
+        from basecount_amd.dist import CommInitAbandoned, CommInitError, Group
 
         try:
             group = Group(ctx=ctx)  # RCCL over xGMI (BASECOUNT_DIST_BACKEND=gloo: rehearsal)
+        except CommInitAbandoned as e:
+            # an init call is still blocked inside RCCL on some rank: no fallback in this process
+            # (the abandoned thread may hold HIP / RCCL locks); every rank ends here, non-zero
+            print(f"bench.py rank {rank}: {e}", file=sys.stderr, flush=True)
+            os._exit(4)
         except CommInitError as e:
-            # the ranks voted (dist.rendezvous_init): every rank is here, so all of them take gloo;
-            # the line says so (config.comm, config.parallelism, config.comm_fallback)
+            # the ranks voted (dist.rendezvous_init): every init call returned and the communicators
+            # that came up were destroyed, so all ranks take gloo together; the line says so (config.comm, config.parallelism, config.comm_fallback)
             print(f"bench.py rank {rank}: RCCL group failed ({e}); every rank falls back to gloo",
                   file=sys.stderr, flush=True)
             group = Group("gloo")
@@ -1177,11 +1316,11 @@ def main():
         head = run_c5(ctx, group, args, rank, world, args.steps, args.warmup, args.launch)
     else:
         head = run_config(args.config, ctx, group, args, rank, world, args.steps, args.warmup, args.launch,
-                          summarise=False)
+                          summarise=args.config == "c4")
     wl = head.pop("_wl")
     # ---- gather of the per-contig summaries to rank 0 (the output step, after the timed region)
     gather_ms = None
-    if group is not None and args.config != "c5":
+    if group is not None and args.config not in ("c4", "c5"):
         payload = []
         for _, L, _, _, o in wl.work:
             work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
@@ -1199,13 +1338,15 @@ def main():
 
     extra = {}
     if not args.no_extras:
-        todo = (["c3", "c5"] if world == 1 else ["c5"])
+        todo = (["c3", "c4", "c5"] if world == 1 else ["c5"])
         for cfg in todo:
             if cfg == args.config:
                 continue
             st, wu = (min(args.steps, 200), min(args.warmup, 20)) if cfg != "c5" else (min(args.steps, 10), 2)
             if cfg == "c5":
                 r = run_c5(ctx, group, args, rank, world, st, wu, args.launch)
+            elif cfg == "c4":  # --summarise-with-bed: kernels 1 + 2, summary and amplicons per step
+                r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=True)
             else:
                 r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=False)
             r.pop("_wl").free()
@@ -1248,6 +1389,8 @@ def main():
                 extra["c3"]["cpu_baseline"] = cpu_baseline(rs3, b3, rs3.lengths[0], budget3, 0, "C3", pa)
                 if "c3_q20" in extra:
                     extra["c3_q20"]["cpu_baseline"] = cpu_baseline(rs3, b3, rs3.lengths[0], budget3, 20, "C3", pa)
+                if "c4" in extra:
+                    extra["c4"]["cpu_baseline"] = cpu_baseline_c4(b3, rs3.lengths[0], pa, budget3)
                 del pa, b3, rs3
         if not args.no_e2e and args.config == "c2":
             e2e_res = e2e("c2")

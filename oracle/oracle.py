@@ -166,6 +166,28 @@ def amplicons(cov, ent, sec, tiles):
     return out
 
 
+def summary_amplicons_py(rows, tiles):
+    """main.py:469-551 as the reference runs it after get_stats (records -> Python lists, then per
+    tile a scan of every position, np.mean / np.median of the window); returns the summary means
+    and the six amplicon vectors.  Used only as the C4 CPU baseline's workload (bench.py)."""
+    coverages = [r[2] for r in rows]
+    entropies = [r[-2] for r in rows]
+    secondary_entropies = [r[-1] for r in rows]
+    avg = (np.mean(coverages), np.mean(entropies), 100 * (len([c for c in coverages if c != 0]) / len(rows)))
+    vecs = [[] for _ in range(6)]
+    for start, end in tiles:
+        cd, ed, sd = [], [], []
+        for j, (c, e, s2) in enumerate(zip(coverages, entropies, secondary_entropies)):
+            if start <= j <= end:
+                cd.append(c)
+                ed.append(e)
+                sd.append(s2)
+        for k, d in enumerate((cd, ed, sd)):
+            vecs[2 * k].append(np.mean(d) if d else -1)
+            vecs[2 * k + 1].append(np.median(d) if d else -1)
+    return avg, vecs
+
+
 def ref_bcount():
     """The reference's own compiled count.bcount (oracle/_ref), or None when not built."""
     hits = glob.glob(os.path.join(HERE, "_ref", "count*.so"))

@@ -140,12 +140,13 @@ def test_cli_world2_same_error_as_single_process(tmp_path):
 
 
 def _comm_worker(path, fail_rank, fail_what):
-    # run by subprocess: the communicator vote with stand-ins for the RCCL id and init
+    # run by subprocess: the communicator vote with stand-ins for the RCCL id, init and destroy
     import time
 
-    from basecount_amd.dist import CommInitError, env, rendezvous_init
+    from basecount_amd.dist import CommInitAbandoned, CommInitError, env, rendezvous_init
 
     world, rank, _ = env()
+    destroyed = []
 
     def make_id():
         if fail_what == "id" and rank == fail_rank:
@@ -160,21 +161,34 @@ def _comm_worker(path, fail_rank, fail_what):
             time.sleep(600)
         return 1000 + rank
 
+    if fail_what == "late" and rank == fail_rank:  # a straggler: arrives after the init timeout
+        time.sleep(5)
     t0 = time.monotonic()
+    code = 0
     try:
-        res = repr(rendezvous_init(rank, world, make_id, init, timeout=30, init_timeout=3))
+        res = repr(rendezvous_init(rank, world, make_id, init, timeout=30, init_timeout=3,
+                                   destroy=destroyed.append))
     except CommInitError as e:
         res = "CommInitError: " + str(e)
+    except CommInitAbandoned as e:  # what bench.py / the CLI do: end the process, non-zero
+        res, code = "CommInitAbandoned: " + str(e), 4
     with open(f"{path}.{rank}", "w") as fh:
-        fh.write(f"{time.monotonic() - t0:.1f} {res}")
+        fh.write(f"{time.monotonic() - t0:.1f} {destroyed!r} {res}")
+    if code:
+        os._exit(code)
 
 
 @pytest.mark.parametrize("fail_rank,fail_what", [(None, None), (1, "init"), (0, "init"), (0, "id"),
-                                                 (1, "hang")])
+                                                 (1, "hang"), (0, "hang"), (2, "late")])
 def test_comm_init_is_agreed_by_every_rank(tmp_path, fail_rank, fail_what):
-    """the RCCL group comes up on every rank or on none.  A failing (or hung)
-    init on one rank makes every rank raise CommInitError within seconds, so the bench's gloo
-    fallback is taken by all ranks alike instead of leaving some in a collective."""
+    """the RCCL group comes up on every rank or on none.
+    * A failing init on one rank makes every rank raise CommInitError within seconds, after the
+      ranks whose init succeeded destroyed their communicator (nothing left behind for the
+      bench's gloo fallback);
+    * an init still blocked at the timeout makes every rank raise CommInitAbandoned instead, and
+      every process exits non-zero within seconds (no fallback next to an abandoned init thread);
+    * a rank that reaches the rendezvous later than the init timeout does not fail the others:
+      rank 0 hands out the id only once every rank is connected."""
     world = 3
     path = tmp_path / "c"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
@@ -183,12 +197,20 @@ def test_comm_init_is_agreed_by_every_rank(tmp_path, fail_rank, fail_what):
             "t._comm_worker(%r, %r, %r)" % (os.path.dirname(HERE), HERE, str(path), fail_rank, fail_what))
     procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
              for r in range(world)]
-    assert [p.wait(timeout=120) for p in procs] == [0] * world
-    res = [(tmp_path / f"c.{r}").read_text().split(" ", 1) for r in range(world)]
-    assert all(float(t) < 20 for t, _ in res)
-    if fail_rank is None:
-        assert [r for _, r in res] == [repr(1000 + r) for r in range(world)]
-    else:
-        assert all(r.startswith("CommInitError") for _, r in res), res
-        if fail_what != "id":
-            assert all(f"rank {fail_rank}" in r for _, r in res), res
+    codes = [p.wait(timeout=120) for p in procs]
+    assert codes == [4 if fail_what == "hang" else 0] * world
+    res = [(tmp_path / f"c.{r}").read_text().split(" ", 2) for r in range(world)]
+    assert all(float(t) < 20 for t, _, _ in res)
+    if fail_rank is None or fail_what == "late":
+        assert [r for _, _, r in res] == [repr(1000 + r) for r in range(world)]
+        assert all(d == "[]" for _, d, _ in res)
+        return
+    want = "CommInitAbandoned" if fail_what == "hang" else "CommInitError"
+    assert all(r.startswith(want) for _, _, r in res), res
+    if fail_what != "id":
+        assert all(f"rank {fail_rank}" in r for _, _, r in res), res
+    # every communicator that did come up was destroyed before the error
+    for r, (_, d, _) in enumerate(res):
+        up = fail_what in ("init", "hang") and r != fail_rank
+        assert d == (f"[{1000 + r}]" if up else "[]"), (r, d)
+

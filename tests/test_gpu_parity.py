@@ -45,7 +45,9 @@ def gpu_count(ctx, b, L, mbq, ncols, **kw):
     return h, bad
 
 
-def random_batch(rng, L, n, long_skip=False, sort=True, nfrac=0.05):
+def random_batch(rng, L, n, long_skip=False, sort=True, nfrac=0.05, starts=None):
+    """n random reads (mixed CIGARs, 5 % non-ACGT letters) on a reference of L positions, starts
+    uniform (or drawn by ``starts(rng, span)``), coordinate-sorted unless ``sort`` is False."""
     pos, cigs, seqs, quals = [], [], [], []
     for _ in range(n):
         ops = []
@@ -69,7 +71,7 @@ def random_batch(rng, L, n, long_skip=False, sort=True, nfrac=0.05):
         codes[rng.random(q) < nfrac] = rng.choice([15, 0, 5, 3])
         seqs.append(codes)
         quals.append(rng.integers(0, 45, q).astype(np.uint8))
-        pos.append(int(rng.integers(0, L - span)))
+        pos.append(int(rng.integers(0, L - span)) if starts is None else int(starts(rng, span)))
         cigs.append(ops)
     return build_batch(pos, cigs, seqs, quals, sort)
 
@@ -132,7 +134,7 @@ def shaped_batch(rng, L, n, templates, nfrac=0.02):
         codes[rng.random(q) < nfrac] = rng.choice([15, 0, 5, 3])
         seqs.append(codes)
         quals.append(rng.integers(0, 45, q).astype(np.uint8))
-        pos.append(int(rng.integers(0, L - span)))
+        pos.append(int(rng.integers(0, L - span)) if starts is None else int(starts(rng, span)))
         cigs.append(ops)
     order = np.argsort(pos, kind="stable")
     pos, cigs = [pos[i] for i in order], [cigs[i] for i in order]
@@ -915,6 +917,92 @@ def test_pileup_summary_matches_separate_calls(ctx, L, n, mbq, show_n):
         ctx.pileup_summary(r, L, mbq, k, nf, nf2, None, None, None, None, None, work.ptr, dout.ptr)
         assert ctx.range_error() == -1
         assert np.array_equal(dout.download(np.float64, 4), s), rep
+
+
+@pytest.mark.parametrize("L,n,mbq,show_n,layout", [
+    (8192 * 64, 6_000, 0, False, "uniform"),
+    (8192 * 64 + 4_321, 6_000, 20, True, "uniform"),
+    (8192 * 200 + 17, 20_000, 0, False, "clusters"),     # hot spots: many leaves two reads share
+    (8192 * 200 + 17, 20_000, 30, True, "clusters"),
+    (8192 * 30, 3_000, 0, False, "boundaries"),          # reads across leaf / quarter / buffer edges
+    (3_000_000, 1_500, 0, False, "uniform"),
+])
+def test_summary_only_read_parallel(ctx, L, n, mbq, show_n, layout):
+    """The summary-only path of a sparse batch (bc_sum.hip: counted positions per 128-position
+    leaf, exact walks of the leaves two reads share, numpy's tree per quarter) gives exactly the
+    four numbers numpy computes over the oracle's coverage and entropies (main.py:469-499), with
+    mixed CIGARs, quality thresholds, N columns, dense clusters and partial last buffers; and
+    again on the same context (its leaf scratch is left zeroed)."""
+    rng = np.random.default_rng(L + n + mbq)
+    if layout == "clusters":
+        centers = rng.integers(0, L - 400, 60)
+        starts = lambda g, span: int(min(L - span - 1, centers[g.integers(0, 60)] + g.integers(0, 300)))
+    elif layout == "boundaries":
+        starts = lambda g, span: int(max(0, min(L - span - 1, 128 * g.integers(1, L // 128) - g.integers(0, 40))))
+    else:
+        starts = None
+    b = random_batch(rng, L, n, starts=starts)
+    k = 6 if show_n else 5
+    nf, nf2 = norm_factors(k)
+    exp, (bad, _) = O.bcount(L, mbq, b)
+    assert bad == -1
+    cov, _, ent, _ = O.stats(exp, show_n)
+    want = np.array([np.mean(cov.astype(np.int64)), np.mean(ent), np.count_nonzero(cov),
+                     cov.astype(np.int64).sum()], np.float64)
+    r = D.DeviceReads(ctx, b)
+    work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+    for rep in range(2):
+        work.zero()
+        ctx.pileup_summary(r, L, mbq, k, nf, nf2, None, None, None, None, None, work.ptr, dout.ptr)
+        assert ctx.range_error() == -1
+        assert np.array_equal(dout.download(np.float64, 4), want), (rep, dout.download(np.float64, 4), want)
+
+
+def test_summary_only_scratch_reuse_across_lengths():
+    """One context, references of decreasing then increasing length with many shared leaves:
+    the leaf scratch (grown once, laid out by its capacity) must be all zero again for each call
+    whatever the previous call's length (a length-dependent layout once read stale slots)."""
+    c = D.Context(0)
+    k = 5
+    nf, nf2 = norm_factors(k)
+    for i, L in enumerate((8192 * 300, 8192 * 12, 8192 * 40 + 3_000, 8192 * 5 + 1, 8192 * 150 + 77)):
+        rng = np.random.default_rng(1234 + i)
+        centers = rng.integers(0, L - 400, 25)
+        starts = lambda g, span: int(min(L - span - 1, centers[g.integers(0, 25)] + g.integers(0, 250)))
+        b = random_batch(rng, L, 4_000 if L > 100_000 else 600, starts=starts)
+        exp, (bad, _) = O.bcount(L, 0, b)
+        cov, _, ent, _ = O.stats(exp, False)
+        want = np.array([np.mean(cov.astype(np.int64)), np.mean(ent), np.count_nonzero(cov),
+                         cov.astype(np.int64).sum()], np.float64)
+        r = D.DeviceReads(c, b)
+        work, dout = c.alloc(D.summary_work_bytes(L)), c.alloc(32)
+        work.zero()
+        c.pileup_summary(r, L, 0, k, nf, nf2, None, None, None, None, None, work.ptr, dout.ptr)
+        assert c.range_error() == -1
+        assert np.array_equal(dout.download(np.float64, 4), want), (L, dout.download(np.float64, 4), want)
+        r.free()
+    c.close()
+
+
+@pytest.mark.parametrize("mbq", [0, 20])
+def test_summary_only_read_parallel_range_error(ctx, mbq):
+    """Reads running past the reference end in the summary-only path: the first offending read
+    is the oracle's (count.cpp:60-65,85, std::out_of_range)."""
+    rng = np.random.default_rng(99 + mbq)
+    L0 = 8192 * 12 + 300
+    b = random_batch(rng, L0, 2_000)
+    w, ob = b["cigar"], b["cig_beg"].astype(np.int64)
+    span = np.array([sum(int(x) >> 4 for x in w[ob[i]: ob[i] + int(b["cig_n"][i])] if int(x) & 15 in (0, 2, 3, 7, 8))
+                     for i in range(b["pos"].size)])
+    e = int((b["pos"].astype(np.int64) + span).max())
+    for L in (e - 20, e - 60, 8192 * 12):
+        _, (bad, _) = O.bcount(L, mbq, b)
+        assert bad >= 0
+        r = D.DeviceReads(ctx, b)
+        work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        ctx.pileup_summary(r, L, mbq, 5, *norm_factors(5), None, None, None, None, None, work.ptr, dout.ptr)
+        assert ctx.range_error() == bad, L
+        r.free()
 
 
 @pytest.mark.parametrize("L,n", [(8192 * 40 + 3_000, 30), (8192 * 3, 0), (5_000_000, 200)])

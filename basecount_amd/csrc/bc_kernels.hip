@@ -859,6 +859,54 @@ __device__ double np_mean_block(const double* a, int64_t n, int* s_off, int* s_l
     return s / (double)n;
 }
 
+// Ascending bitonic sort of 64 * E unsigned 64-bit keys by ONE wave, E per lane (element
+// lane * E + r in register r), no barriers: pairs less than E apart are in one lane's registers,
+// the others E * m apart are lanes m apart (one 64-bit shuffle per key).  Fully unrolled.
+template <int E>
+__device__ __forceinline__ void wave_bitonic(unsigned long long (&v)[E]) {
+    const int lane = threadIdx.x & 63;
+    constexpr int N = 64 * E;
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= E) {
+                const int m = j / E;
+                const bool lower = (lane & m) == 0;
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    const unsigned long long p = __shfl_xor(v[r], m);
+                    const bool up = ((lane * E + r) & k) == 0;
+                    const unsigned long long lo = v[r] < p ? v[r] : p, hi = v[r] < p ? p : v[r];
+                    v[r] = (up == lower) ? lo : hi;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    if (r & j) continue;
+                    const bool up = ((lane * E + r) & k) == 0;
+                    const unsigned long long a = v[r], b = v[r ^ j];
+                    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+                    v[r] = up ? lo : hi;
+                    v[r ^ j] = up ? hi : lo;
+                }
+            }
+        }
+    }
+}
+// The k-th smallest of a wave's sorted keys (k < 64 * E, wave-uniform)
+template <int E>
+__device__ __forceinline__ unsigned long long wave_kth(const unsigned long long (&v)[E], int64_t k) {
+    const int r = (int)(k % E), l = (int)(k / E);
+    unsigned long long x = v[0];
+#pragma unroll
+    for (int i = 1; i < E; ++i) x = r == i ? v[i] : x;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+constexpr int kAmpSortE = 8;  // windows of <= 512 positions: medians by one wave's bitonic sort
+
 __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const double* ent, const double* sec, int64_t L,
                                                   const int64_t* lo_a, const int64_t* hi_a, double* out) {
     __shared__ unsigned s_hist[256];
@@ -877,23 +925,52 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
         return;
     }
     const int64_t n = hi - lo + 1;
+    const int64_t k1 = (n - 1) / 2, k2 = n / 2;
+    __shared__ unsigned long long s_med[3][2];  // the k1-th / k2-th smallest of cov, ent, sec
+    if (n <= 64 * kAmpSortE) {
+        // windows of amplicon size (C4: ~300 positions): waves 0-2 each sort one array's keys in
+        // registers (the doubles are >= 0, so their bit patterns order like their values)
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (wave < 3) {
+            unsigned long long v[kAmpSortE];
+#pragma unroll
+            for (int r = 0; r < kAmpSortE; ++r) {  // (coalesced: the input order does not matter)
+                const int64_t i = (int64_t)r * 64 + lane;
+                v[r] = ~0ull;
+                if (i < n)
+                    v[r] = wave == 0 ? (unsigned long long)(uint32_t)cov[lo + i]
+                                     : (unsigned long long)__double_as_longlong((wave == 1 ? ent : sec)[lo + i]);
+            }
+            wave_bitonic<kAmpSortE>(v);
+            const unsigned long long a = wave_kth<kAmpSortE>(v, k1), b = wave_kth<kAmpSortE>(v, k2);
+            if (lane == 0) {
+                s_med[wave][0] = a;
+                s_med[wave][1] = b;
+            }
+        }
+        __syncthreads();
+    }
     // coverage: exact integer mean, median via 32-bit select
     long long cs = 0;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) cs += cov[lo + i];
     cs = block_sum_i64(cs, s_red);
-    const int64_t k1 = (n - 1) / 2, k2 = n / 2;
+    const bool sorted = n <= 64 * kAmpSortE;  // (uniform)
     auto ckey = [&](int64_t i) { return (unsigned long long)(uint32_t)cov[lo + i]; };
-    const double c_a = (double)radix_select(ckey, n, k1, 32, s_hist, s_sel);
-    const double c_b = (k2 != k1) ? (double)radix_select(ckey, n, k2, 32, s_hist, s_sel) : c_a;
+    const double c_a = sorted ? (double)s_med[0][0] : (double)radix_select(ckey, n, k1, 32, s_hist, s_sel);
+    const double c_b = sorted ? (double)s_med[0][1]
+                              : (k2 != k1) ? (double)radix_select(ckey, n, k2, 32, s_hist, s_sel) : c_a;
     const double* vals[2] = {ent + lo, sec + lo};
     double means[2], meds[2];
     for (int q = 0; q < 2; ++q) {
         const double* a = vals[q];
         means[q] = np_mean_block(a, n, s_off, s_len, s_val);
         auto dkey = [&](int64_t i) { return (unsigned long long)__double_as_longlong(a[i]); };
-        const double va = __longlong_as_double((long long)radix_select(dkey, n, k1, 64, s_hist, s_sel));
-        const double vb =
-            (k2 != k1) ? __longlong_as_double((long long)radix_select(dkey, n, k2, 64, s_hist, s_sel)) : va;
+        const double va = __longlong_as_double(
+            (long long)(sorted ? s_med[1 + q][0] : radix_select(dkey, n, k1, 64, s_hist, s_sel)));
+        const double vb = __longlong_as_double(
+            (long long)(sorted ? s_med[1 + q][1]
+                               : (k2 != k1) ? radix_select(dkey, n, k2, 64, s_hist, s_sel)
+                                            : (unsigned long long)__double_as_longlong(va)));
         meds[q] = (k2 != k1) ? ((0.0 + va) + vb) / 2.0 : (0.0 + va) / 1.0;
     }
     if (threadIdx.x == 0) {

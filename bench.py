@@ -1445,6 +1445,12 @@ def main():
         if "serial_us_per_step" in head:
             line["serial_us_per_step"] = head["serial_us_per_step"]
             line["serial_device_us_per_step"] = head.get("serial_device_us_per_step")
+        # the headline step from a raw batch: index build + k_pileup, k_pileup
+        # searching pos[], and the indexed step, all serialized device time per step
+        for key in ("raw_step_us", "no_index_step_us", "indexed_step_us", "index_us", "pileup_frac_without_index",
+                    "step_input"):
+            if key in head:
+                line[key] = head[key]
         if cpu:
             line["speedup_vs_cpu"] = head["value"] / cpu["value"]
             line["speedup_vs_cpu_all_cores"] = head["value"] / cpu_all["value"]

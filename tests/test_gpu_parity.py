@@ -692,14 +692,20 @@ def test_summary_matches_numpy(ctx, L):
     assert int(s[2]) == int(np.count_nonzero(cov))
 
 
-def test_amplicons_match_numpy(ctx):
-    rng = np.random.default_rng(3)
+@pytest.mark.parametrize("wmax,ties", [(9000, False), (600, True)])
+def test_amplicons_match_numpy(ctx, wmax, ties):
+    """k_amplicon against numpy's mean / median per window (main.py:519-551): wide windows (the
+    radix-select medians) and amplicon-sized ones (<= 512 positions: one wave's bitonic sort per
+    array), with many tied values, odd and even lengths, empty and clipped windows."""
+    rng = np.random.default_rng(3 + wmax)
     L = 30_000
-    cov = rng.integers(0, 3000, L).astype(np.int32)
-    ent = rng.random(L)
+    cov = rng.integers(0, 6 if ties else 3000, L).astype(np.int32)
+    ent = rng.integers(0, 4, L) / 3.0 if ties else rng.random(L)
     sec = rng.random(L)
+    if ties:
+        sec[rng.random(L) < 0.5] = 1.0
     ent[:500] = 1.0
-    tiles = [(int(a), int(a + w)) for a, w in zip(rng.integers(-50, L, 200), rng.integers(-5, 9000, 200))]
+    tiles = [(int(a), int(a + w)) for a, w in zip(rng.integers(-50, L, 200), rng.integers(-5, wmax, 200))]
     tiles += [(0, 0), (L - 1, L + 10), (5, 4), (L + 5, L + 9), (0, L - 1)]
     lo = np.array([t[0] for t in tiles], np.int64)
     hi = np.array([t[1] for t in tiles], np.int64)

@@ -243,6 +243,19 @@ int bc_ctx_destroy(bc_ctx* c) {
     return BC_OK;
 }
 
+int bc_ctx_release_scratch(bc_ctx* c) {
+    if (!c) return fail(BC_E_ARG, "ctx is NULL");
+    DeviceGuard g(c->device);
+    if (c->rc_scratch || c->out_scratch || c->sum_scratch) HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->rc_scratch) HIP_TRY(hipFree(c->rc_scratch));
+    if (c->out_scratch) HIP_TRY(hipFree(c->out_scratch));
+    if (c->sum_scratch) HIP_TRY(hipFree(c->sum_scratch));
+    c->rc_scratch = nullptr;
+    c->out_scratch = c->sum_scratch = nullptr;
+    c->rc_scratch_bytes = c->out_scratch_bytes = c->sum_scratch_bytes = 0;
+    return BC_OK;
+}
+
 int bc_ctx_stream(bc_ctx* c, void** s) {
     if (!c || !s) return fail(BC_E_ARG, "NULL argument");
     *s = (void*)c->stream;
@@ -618,7 +631,9 @@ int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, in
             const int32_t* cov_base = (const int32_t*)((uintptr_t)parts.cov_tail - (uintptr_t)off * 4u);
             const double* ent_base = (const double*)((uintptr_t)parts.ent_tail - (uintptr_t)off * 8u);
             Timed tm(c, BC_K_SUMMARY);
-            HIP_TRY(bc::launch_summary_partials(c->stream, cov_base, ent_base, L, d_work, parts.full_chunks));
+            // (the read-parallel summary writes whole-buffer partials, the sweep quarter ones)
+            HIP_TRY(bc::launch_summary_partials(c->stream, cov_base, ent_base, L, d_work, parts.full_chunks,
+                                                !parts.whole_buffers));
             return BC_OK;
         }
         // counts [k][L] int32, cov [L] int32, ent / sec [L] double

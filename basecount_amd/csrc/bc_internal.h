@@ -82,6 +82,7 @@ struct SumParts {
     // 8192; at most 8192 positions) for the fold's last partial buffer.  Honoured only when the
     // sweep fuses the partials (out: fused); otherwise the caller must give full outputs.
     bool no_store = false;
+    bool whole_buffers = false;  // (out) the partials of [0, full_chunks) are per buffer, not per quarter
     int32_t* cov_tail = nullptr;
     double* ent_tail = nullptr;
 };
@@ -145,8 +146,9 @@ hipError_t launch_index(hipStream_t s, bc_reads& r, const IndexPlan& plan, void*
 size_t summary_work_bytes(int64_t L);
 hipError_t launch_summary(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
                           double* out, int64_t first_chunk = 0);
+// (quarters: the buffers before first_chunk come as quarter partials, else as whole-buffer ones)
 hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
-                                   int64_t first_chunk);
+                                   int64_t first_chunk, bool quarters = true);
 // (the work buffers' headers say which leading buffers come as quarters)
 hipError_t launch_summary_fold(hipStream_t s, int n, const int64_t* L, void* const* work, double* const* out);
 // the partial arrays inside a summary work buffer

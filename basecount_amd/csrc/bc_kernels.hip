@@ -707,12 +707,17 @@ __global__ __launch_bounds__(256) void k_sum_tail(const int32_t* cov, const doub
 }
 
 // The float64 fold over the per-buffer partials stays sequential (numpy adds the buffers'
-// pairwise sums in order: one dependent add per buffer is the floor).  One workgroup per
+// pairwise sums in order), but it need not take one dependent add per buffer.  Buffer sums are
+// >= 0, and most are integers (8192 positions whose entropies are 0.0 / 1.0: every buffer no two
+// reads share a position of; exactly 8192.0 without reads).  Adding integers to s rounds only
+// where s crosses into a binade whose ulp exceeds the granularity of its fraction, and then the
+// final sum of the run is not representable either: so a run of integer buffers adds as ONE add
+// of its exact integer total whenever that add is exact (TwoSum error 0), and only fractional
+// buffers (and the rare run that crosses such a binade) take sequential adds.  One workgroup per
 // reference, so the folds of several references (bc_summary_fold) run side by side.  The
 // partials are double-buffered through LDS, 1024 per round: the block loads round r+1 into
-// registers while thread 0 folds round r from LDS in groups of 8 (loads of a group issued
-// together), so the fold never waits on a global load.  The integer sums are order-free and
-// reduce in parallel.
+// registers while round r is scanned (the integer buffers' exact prefix sums and the list of the
+// fractional ones) and folded by thread 0 from LDS.  The integer sums reduce in parallel.
 struct FoldRef {
     const double* pe;
     const long long* pc;
@@ -730,25 +735,38 @@ struct FoldArgs {
     FoldRef ref[kFoldMax];
 };
 
-__global__ __launch_bounds__(256) void k_sum_final(FoldArgs FA) {
-    constexpr int kR = 1024;
-    __shared__ double s_buf[2][kR];
-    __shared__ long long s_red[8];
+constexpr int kFoldThreads = 1024;
+__global__ __launch_bounds__(kFoldThreads) void k_sum_final(FoldArgs FA) {
+    constexpr int kR = 4 * kFoldThreads;  // buffers per round, 4 per thread
+    constexpr int kW = kFoldThreads / 64;
+    __shared__ double s_buf[kR];
+    // The walk (rounds with at most kE fractional buffers): per fractional buffer, in order, its
+    // index, the exclusive prefix of the round's integer buffer sums (<= 8192 each) before it, its
+    // value, and the running sum s before its run (the optimistic chain's record)
+    constexpr int kE = kR / 4;
+    constexpr int kB = 8;  // events per batch of the chain
+    __shared__ uint16_t s_fr[kE];
+    __shared__ int s_fpre[kE + 1 + kB];   // (past the last event: the round's total, repeated)
+    __shared__ double s_fv[kE + 1 + kB];  // (past the last fractional buffer: 0.0)
+    __shared__ double s_rd[kE + 1 + kB];  // each event's integer run total, as a double (exact)
+    __shared__ int s_total;  // the round's integer buffer sum
+    __shared__ int s_wsum[kW], s_wfr[kW];
+    __shared__ long long s_red[2 * kW];
     const FoldRef& R = FA.ref[blockIdx.x];
     const double* part_ent = R.pe;
     const long long* part_cov = R.pc;
     const long long* part_nz = R.pn;
     const int64_t nchunks = R.nchunks;
     const int64_t nq = *R.nquart;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     double s = 0.0;
     long long cs = 0, nz = 0;
     double v[4];
     long long vc[4], vn[4];
-    auto load = [&](int64_t r0) {  // issue only: the values are consumed after the fold
+    auto load = [&](int64_t r0) {  // issue only: the values are consumed a round later
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int64_t c = r0 + t + 256 * j;
+            const int64_t c = r0 + t + kFoldThreads * j;
             if (c < nq) {  // a buffer's 4 quarters: (q0 + q1) + (q2 + q3), numpy's tree
                 const double* q = R.qe + 4 * c;
                 v[j] = (q[0] + q[1]) + (q[2] + q[3]);
@@ -762,50 +780,155 @@ __global__ __launch_bounds__(256) void k_sum_final(FoldArgs FA) {
             }
         }
     };
-    auto stash = [&](int buf) {
+    auto stash = [&]() {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            s_buf[buf][t + 256 * j] = v[j];
+            s_buf[t + kFoldThreads * j] = v[j];
             cs += vc[j];
             nz += vn[j];
         }
     };
+    // the round's scan: thread t takes buffers 4t .. 4t+3 (in order); integer sums as int (a
+    // round's total <= 4096 * 8192), fractional buffers listed in order
+    auto scan = [&](int m) {
+        int isum = 0, nfr = 0, iv[4];
+        bool fr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * t + j;
+            const double x = e < m ? s_buf[e] : 0.0;
+            fr[j] = e < m && x != __builtin_floor(x);
+            iv[j] = fr[j] ? 0 : (int)x;
+            isum += iv[j];
+            nfr += fr[j] ? 1 : 0;
+        }
+        int ps = isum, pf = nfr;  // inclusive wave scans
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int a = __shfl_up(ps, o), f = __shfl_up(pf, o);
+            if (lane >= o) ps += a, pf += f;
+        }
+        if (lane == 63) s_wsum[wave] = ps, s_wfr[wave] = pf;
+        __syncthreads();
+        int bs = 0, bf = 0, tf = 0;
+        for (int w = 0; w < kW; ++w) {
+            if (w < wave) bs += s_wsum[w], bf += s_wfr[w];
+            tf += s_wfr[w];
+        }
+        int xs = bs + ps - isum, xf = bf + pf - nfr;  // exclusive
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * t + j;
+            if (fr[j]) {
+                if (xf < kE) {
+                    s_fr[xf] = (uint16_t)e;
+                    s_fpre[xf] = xs;
+                    s_fv[xf] = s_buf[e];
+                }
+                ++xf;
+            }
+            xs += iv[j];
+        }
+        if (t == kFoldThreads - 1) s_total = xs;
+        __syncthreads();
+        return tf;
+    };
     load(0);
-    stash(0);
+    stash();
     __syncthreads();
-    int cur = 0;
     for (int64_t r0 = 0; r0 < nchunks; r0 += kR) {
         const bool more = r0 + kR < nchunks;
-        if (more) load(r0 + kR);  // in flight while thread 0 folds this round
-        if (t == 0) {
-            const int m = (int)((nchunks - r0) < kR ? (nchunks - r0) : kR);
-            const double* b = s_buf[cur];
-            int i = 0;
-            for (; i + 8 <= m; i += 8) {
-                double w[8];
+        if (more) load(r0 + kR);  // in flight while this round is scanned and folded
+        const int m = (int)((nchunks - r0) < kR ? (nchunks - r0) : kR);
+        const int nfr = scan(m);
+        const bool walk = nfr <= kE && 4 * nfr <= m;  // (uniform) few fractional buffers: the event walk
+        if (!walk) {
+            if (t == 0) {  // mostly fractional: plain sequential adds
+                const double* b = s_buf;
+                int i = 0;
+                for (; i + 8 <= m; i += 8) {
+                    double w[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) w[u] = b[i + u];
+                    for (int u = 0; u < 8; ++u) w[u] = b[i + u];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) s += w[u];
+                    for (int u = 0; u < 8; ++u) s += w[u];
+                }
+                for (; i < m; ++i) s += b[i];
             }
-            for (; i < m; ++i) s += b[i];
+        } else {
+            // Each fractional buffer f ends an integer run of exact total R_f (prefix difference;
+            // event nfr: the round's last run): s = (s + R_f) + v_f, two adds per event, by thread
+            // 0 alone.  The run's add (and every partial sum inside it, all smaller) is exact when
+            // s + R_f lies in the binade of s (multiples of ulp(s) <= 1): checked with integer ops
+            // on the exponent bits, off the add chain, per batch of kB events (loads of the next
+            // batch in flight); a batch with a run leaving its binade (a few per reference) is
+            // redone buffer by buffer from the s before it.
+            if (t <= kB) {  // the last run and the batch padding: x unchanged past it
+                s_fpre[nfr + t] = s_total;
+                s_fv[nfr + t] = 0.0;
+            }
+            __syncthreads();
+            for (int f = t; f <= nfr + kB; f += kFoldThreads)
+                s_rd[f] = (double)(s_fpre[f] - (f ? s_fpre[f - 1] : 0));
+            __syncthreads();
+            if (t == 0) {
+                auto hi = [](double v) { return (uint32_t)((unsigned long long)__double_as_longlong(v) >> 32); };
+                double x = s, rdA[kB], fvA[kB];
+#pragma unroll
+                for (int u = 0; u < kB; ++u) rdA[u] = s_rd[u], fvA[u] = s_fv[u];
+                for (int f0 = 0; f0 <= nfr; f0 += kB) {
+                    double rdB[kB], fvB[kB];
+                    const int fn = f0 + kB <= nfr ? f0 + kB : f0;  // (the next batch, or a reload)
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) rdB[u] = s_rd[fn + u], fvB[u] = s_fv[fn + u];
+                    const double x0 = x;
+                    uint32_t moved = 0;
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) {
+                        const double tt = x + rdA[u];
+                        moved |= (hi(x) ^ hi(tt)) & 0xFFF00000u;  // the exponent changed
+                        x = tt + fvA[u];  // (past the last event: + 0.0 + 0.0, exact)
+                    }
+                    // (a batch of integer buffers only, from an integer-valued s: exact below 2^53)
+                    if (moved && !(f0 == nfr && x0 == __builtin_floor(x0) && x < 9007199254740992.0)) {
+                        // redo the batch's buffers one by one, loaded 8 at a time
+                        const int last = f0 + kB - 1 < nfr ? f0 + kB - 1 : nfr;
+                        const int i0 = f0 == 0 ? 0 : (int)s_fr[f0 - 1] + 1;
+                        const int i1 = last < nfr ? (int)s_fr[last] + 1 : m;
+                        x = x0;
+                        int i = i0;
+                        for (; i + 8 <= i1; i += 8) {
+                            double w[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) w[u] = s_buf[i + u];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) x += w[u];
+                        }
+                        for (; i < i1; ++i) x += s_buf[i];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) rdA[u] = rdB[u], fvA[u] = fvB[u];
+                }
+                s = x;
+            }
         }
-        if (more) stash(cur ^ 1);
+        __syncthreads();  // s_buf read by thread 0
+        if (more) stash();
         __syncthreads();
-        cur ^= 1;
     }
     for (int o = 32; o > 0; o >>= 1) {
         cs += __shfl_down(cs, o);
         nz += __shfl_down(nz, o);
     }
-    if ((t & 63) == 0) {
-        s_red[t >> 6] = cs;
-        s_red[4 + (t >> 6)] = nz;
+    if (lane == 0) {
+        s_red[wave] = cs;
+        s_red[kW + wave] = nz;
     }
     __syncthreads();
     if (t == 0) {
-        cs = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-        nz = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
+        cs = 0;
+        nz = 0;
+        for (int w = 0; w < kW; ++w) cs += s_red[w], nz += s_red[kW + w];
         const double n = (double)R.L;
         R.out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
         R.out[1] = s / n;
@@ -1103,11 +1226,11 @@ SumParts summary_parts(void* work, int64_t L) {
 // first_chunk > 0: the partials of the buffers before it are already in the work buffer (written
 // by the sparse pileup sweep, bc_pileup_summary); only the rest are computed here
 hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const double* ent, int64_t L, void* work,
-                                   int64_t first_chunk) {
+                                   int64_t first_chunk, bool quarters) {
     const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
     const SumParts P = summary_parts(work, L);
     // the header tells the fold how many leading buffers come as quarters (stream-ordered)
-    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)P.hdr, (int)first_chunk, 1, s);
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)P.hdr, quarters ? (int)first_chunk : 0, 1, s);
     if (e != hipSuccess) return e;
     const int64_t nfull = L / kNpBuf;  // whole buffers: k_sum_chunks; the partial one: k_sum_tail
     if (nfull > first_chunk)
@@ -1129,7 +1252,7 @@ hipError_t launch_summary_fold(hipStream_t s, int n, const int64_t* L, void* con
             FA.ref[i] = FoldRef{P.ent,    P.cov,  P.nz, P.sub_ent, P.sub_cov, P.sub_nz,
                                 P.hdr,    (L[i0 + i] + kNpBuf - 1) / kNpBuf, L[i0 + i], out[i0 + i]};
         }
-        hipLaunchKernelGGL(k_sum_final, dim3((unsigned)m), dim3(256), 0, s, FA);
+        hipLaunchKernelGGL(k_sum_final, dim3((unsigned)m), dim3(kFoldThreads), 0, s, FA);
     }
     return hipGetLastError();
 }

@@ -61,29 +61,6 @@ constexpr int kWaitVm0 = 0x0F70;
 #define BC_RC_EARLY_WAIT 1
 #endif
 constexpr bool kEarlyWait = BC_RC_EARLY_WAIT != 0;
-// chunk bounds without the index reduced across the waves at the stage barrier (see `deferred`):
-// measured slower (A/B, round 4: 44.2 vs 43.3 us single pass, and the indexed path 35.3 vs 33.4 us
-// from the larger kernel), so off; -DBC_RC_DEFER_BOUNDS=1 builds that variant
-#ifndef BC_RC_DEFER_BOUNDS
-#define BC_RC_DEFER_BOUNDS 0
-#endif
-constexpr bool kDeferBounds = BC_RC_DEFER_BOUNDS != 0;
-// CIGAR words of the next chunk requested at the start of a chunk's image phase (fields kept two
-// chunks ahead) instead of after its expansion: measured slower on C3 (single-pass k_rc 44.2 vs
-// 43.2 µs over 3 A/B pairs: the longer-lived registers cost more than the earlier loads save), so
-// off; -DBC_RC_PF2=1 builds that variant
-#ifndef BC_RC_PF2
-#define BC_RC_PF2 0
-#endif
-constexpr bool kPf2 = BC_RC_PF2 != 0;
-// reads per chunk chosen so that every resident block takes the same number of chunks (launch_rc):
-// measured slower (C3: 6 rounds of 218-read chunks 48.3 us against 5 rounds of 256 + a 67-chunk
-// tail 42.4 us; a round costs ~8.2 us whatever its reads, scripts/reads_sweep.sh), so off;
-// -DBC_RC_BALANCE=1 builds that variant
-#ifndef BC_RC_BALANCE
-#define BC_RC_BALANCE 0
-#endif
-constexpr bool kRcBalance = BC_RC_BALANCE != 0;
 // gather staging of chunks whose sequence is not one short segment (see `gather`); -DBC_RC_GATHER=0
 // builds the variant that walks such chunks from HBM
 #ifndef BC_RC_GATHER
@@ -92,17 +69,6 @@ constexpr bool kRcBalance = BC_RC_BALANCE != 0;
 constexpr bool kGather = BC_RC_GATHER != 0;
 constexpr int kRcSlot = 76;  // stage bytes per read in gather staging (152 nibbles: 150-bp reads at either parity)
 static_assert(kRcSlot % 4 == 0 && kRcSlot * kRcChunk <= 78 * kRcChunk, "gather slots fit the stage");
-// the next chunk's fields requested at the chunk's start (behind its stage copy) instead of after
-// the stage barrier: no measurable change (C3 single pass 45.5-46.1 vs 45.8-45.9 us, A/B x3), so
-// off; -DBC_RC_FIELDS_EARLY=1 builds that variant
-#ifndef BC_RC_FIELDS_EARLY
-#define BC_RC_FIELDS_EARLY 0
-#endif
-constexpr bool kFieldsEarly = BC_RC_FIELDS_EARLY != 0;
-#ifndef BC_RC_IGNORE_RECORDS
-#define BC_RC_IGNORE_RECORDS 0
-#endif
-
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
 constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
 
@@ -235,8 +201,7 @@ struct RcArgs {
 // waves.  Lane k of each wave stores slot k (one masked store, not one per slot); every thread
 // then reads the waves' rows as 16-byte words.  Must be called by the whole block.
 // wave_partials (each wave's results into its row of red) + a barrier + block_combine (every thread
-// folds the rows); k_rc calls the two halves around its stage barrier when it can (no extra
-// barrier in the chunk chain).
+// folds the rows).
 template <int NV>
 __device__ __forceinline__ void wave_partials(const uint32_t (&v)[NV], const bool (&is_max)[NV], uint32_t (*red)[8]) {
     static_assert(NV <= 8, "one 8-word row per wave");
@@ -361,13 +326,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // run records (bc_reads.read_runs) in place of the first decode: the variants with spare
     // registers (the others spill with the extra path)
     constexpr bool kRunsOn = !QUAL && NC == 5;
-    // A/B only (-DBC_RC_IGNORE_RECORDS=1): decode the CIGARs but take the chunk summaries
-    constexpr bool kRecordsOn = kRunsOn && !BC_RC_IGNORE_RECORDS;
     // the next chunk's per-read fields are loaded while the current one is walked
     uint32_t fpos = 0x7FFFFFFFu, fsn = 0, fcb = 0, fcn = 0, fsn_first = 0, fsn_last = 0;
-    // kPf2 (CIGAR decode without the index): the fields one chunk further ahead (g*), so that the
-    // next chunk's CIGAR words can be requested as soon as a chunk's image phase begins
-    uint32_t gpos = 0x7FFFFFFFu, gsn = 0, gcb = 0, gcn = 0, gsn_first = 0, gsn_last = 0;
     auto fetch_into = [&](IT ch, uint32_t& xpos, uint32_t& xsn, uint32_t& xcb, uint32_t& xcn, uint32_t& xfirst,
                           uint32_t& xlast) {
         if (ch >= n_chunks) return;
@@ -375,7 +335,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const int n = (int)(n_reads - b0 < CR ? n_reads - b0 : CR);
         if (tid < n) {
             xpos = (uint32_t)*elem(A.pos, b0 + tid);
-            if (!kRecordsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
+            if (!kRunsOn || !A.runs) {  // (uniform) with run records the CIGAR is read only on demand
                 xcb = *elem(A.cig_beg, b0 + tid);
                 xcn = *elem(A.cig_n, b0 + tid);
             }
@@ -386,12 +346,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     };
     auto fetch_fields = [&](IT ch) { fetch_into(ch, fpos, fsn, fcb, fcn, fsn_first, fsn_last); };
     fetch_fields((IT)blockIdx.x);
-    const bool pf2 = kPf2 && !(kRecordsOn && A.runs);  // (uniform)
-    if (pf2) fetch_into((IT)blockIdx.x + (IT)gridDim.x, gpos, gsn, gcb, gcn, gsn_first, gsn_last);
     // the next chunk's first CIGAR words, loaded during this chunk's sum (pf_ok: loaded); not
     // with qualities and six columns, which sit at the VGPR cap without it
     constexpr bool kPfOn = !(QUAL && NC == 6);
-    const uint4* const runs = kRecordsOn ? A.runs : nullptr;
+    const uint4* const runs = kRunsOn ? A.runs : nullptr;
     // the upload's chunk summaries: the chunk bounds without the block reduction (and its barrier)
     const uint4* const sums = kRunsOn && A.runs ? A.sums : nullptr;
     if (tid < 2) ncx[tid] = 0;
@@ -451,10 +409,6 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // the copy's round trip).  They were issued a whole phase ago: this wait is ~free.
         if (kEarlyWait) __builtin_amdgcn_s_waitcnt(kWaitVm0);
         if (spec) stage_dma<kRcThreads>(stage, A.seq + spec_lo, spec_hi - spec_lo, tid);
-        // (kFieldsEarly) the next chunk's fields requested behind the stage copy, so they have
-        // arrived when its CIGAR words are prefetched after the stage barrier
-        const bool fields_early = kFieldsEarly && kPfOn && !kPf2 && !(kRecordsOn && A.runs);  // (uniform)
-        if (fields_early) fetch_fields(chunk + (IT)gridDim.x);
         RunTable T;
         T.nrun = 0;
         T.gap = T.complex = false;
@@ -533,18 +487,15 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             }
             cspan = sp > 0x3FFFFFFFu ? 0x3FFFFFFFu : (uint32_t)sp;
         }
-        uint32_t v[7];
-        const bool is_max[7] = {false, true, false, true, true, true, true};
-        // (uniform) without the index's summaries and qualities: each wave reduces its share of the
-        // chunk bounds now and the block combines them after the stage barrier, assuming the
-        // speculative stage and the event image (a chunk for which either is wrong restages /
-        // writes run tables after that barrier and meets at a second one): the chunk chain has no
-        // barrier more than with the summaries
-        const bool deferred = !sums && !QUAL && kDeferBounds;
+        // v[7]: the longest simple read's sequence bytes (gather staging's slot test; not in the
+        // upload's summaries, whose chunks never take gather staging)
+        uint32_t v[8];
+        const bool is_max[8] = {false, true, false, true, true, true, true, true};
         if (sums) {  // (uniform) reduced by the upload (bc_capi.hip chunk_summary: the same values)
             const uint32_t* sw = (const uint32_t*)elem(sums, 2 * chunk);
 #pragma unroll
             for (int k = 0; k < 7; ++k) v[k] = sload(sw + k);
+            v[7] = 0u;
             RC_STAMP(1);
             RC_STAMP(2);
         } else {
@@ -557,16 +508,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             // at its end) count as 3 runs: such a chunk takes the run tables
             v[5] = simple ? run_shape(T) : 0u;
             v[6] = (simple && T.gap) ? 1u : 0u;
+            v[7] = simple ? (((msn & 1u) + T.qlen + 1u) >> 1) : 0u;
             RC_STAMP(1);
-            if (deferred) {
-                wave_partials<7>(v, is_max, red);
-                if (cx) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
-                stage_wait();     // this thread's speculative LDS-DMA landed
-                __syncthreads();  // the stage, the complex-read list and the waves' partial bounds
-                block_combine<7, kRcWaves>(v, is_max, red);
-            } else {
-                block_reduce<7, kRcWaves>(v, is_max, red);  // contains a __syncthreads
-            }
+            block_reduce<8, kRcWaves>(v, is_max, red);  // contains a __syncthreads
             RC_STAMP(2);
         }
         const IT P0 = (IT)v[0], P1 = (IT)v[1];
@@ -586,13 +530,17 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // sorted on the device without relaying its sequence, bc_sort.hip): every simple read's
         // bytes are copied to its own kRcSlot-byte slot of the stage instead, and a read longer
         // than its slot is walked as a complex read (rc_complex, from HBM).
-        const bool gather = kGather && !QUAL && !deferred && !staged && !sums && !(BC_ABL(A) & 512);  // (uniform)
+        // Only when every simple read fits its slot (a chunk of long reads would walk
+        // most of them as complex reads, one per wave with global atomics, where the run-table walk
+        // from HBM is the better fallback).
+        const bool gather = kGather && !QUAL && !staged && !sums && v[7] <= (uint32_t)kRcSlot &&
+                            !(BC_ABL(A) & 512);  // (uniform)
         const bool big = gather && simple && ((((msn & 1u) + T.qlen + 1u) >> 1) > (uint32_t)kRcSlot);
         const bool cxa = cx || big, simplea = simple && !big;
         const bool inlds = staged || gather;  // (uniform) the walks read the stage
         // the read's first base as a nibble index of the stage (or of the batch's buffer)
         const uint32_t rel = gather ? (uint32_t)(2 * kRcSlot * tid) + (msn & 1u) : msn - (staged ? 2u * seg_lo : 0u);
-        if (cxa && !deferred) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
+        if (cxa) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         // event-image path: a staged chunk of reads with <= 2 runs whose windows fit the image.
         // Each read's events are extracted ONCE per window (lane = read, its windows in a row)
         // instead of once per (window, run) item from the run table.
@@ -601,7 +549,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const bool img_path = inlds && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
         const int gpad = NWc;  // (uniform) the image's group padding (see rec)
         uint32_t* const mycol = img + tid * kImgRows + (tid >> 5) * gpad;  // this read's image column
-        if (spec && !spec_ok && !deferred) {  // (uniform) the speculative copy is overwritten
+        if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
             stage_wait();
             __syncthreads();
         }
@@ -663,31 +611,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             }
             if (!img_path) rpos[tid] = (int32_t)mpos;  // (the window tables of the run-table walk)
         }
-        if (!deferred || !spec_ok || !img_path) {  // (uniform) deferred: only a chunk that restaged or wrote records
-            if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
-            __syncthreads();  // stage, records and the complex-read list complete
-        }
+        if (!QUAL) stage_wait();  // this thread's LDS-DMA landed (hipcc does not track it)
+        __syncthreads();  // stage, records and the complex-read list complete
         RC_STAMP(3);
-        bool pf_early = false;
-        if (kPfOn && pf2) {
-            // the next chunk's fields arrived during this one (g*): its CIGAR words are requested
-            // now, a whole image phase earlier than below, and the fields of the chunk after it
-            // are fetched into g*
-            fpos = gpos, fsn = gsn, fcb = gcb, fcn = gcn, fsn_first = gsn_first, fsn_last = gsn_last;
-            fetch_into(chunk + 2 * (IT)gridDim.x, gpos, gsn, gcb, gcn, gsn_first, gsn_last);
-            if (chunk + (IT)gridDim.x < n_chunks) {
-                const IT nb0 = (chunk + (IT)gridDim.x) * CR;
-                const int nn = (int)(n_reads - nb0 < CR ? n_reads - nb0 : CR);
-                const bool nv = tid < nn;
-                const int ncm = (BC_ABL(A) & 262144) ? 0 :  // diagnostic: no CIGAR prefetch
-                                    (int)U(wave_reduce<true>(nv ? (fcn < (uint32_t)kPre ? fcn : (uint32_t)kPre) : 0u));
-#pragma unroll
-                for (int i = 0; i < kPf; ++i) pw[i] = (nv && i < ncm && (uint32_t)i < fcn) ? A.cigar[fcb + i] : 0u;
-                pf_early = true;
-            }
-        } else if (kPfOn) {
-            if (!fields_early) fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
-        }
+        if (kPfOn) fetch_fields(chunk + (IT)gridDim.x);  // back before the CIGAR prefetch below
         if (img_path) {
             // ---- event image: thread tid writes column tid, rows = the chunk's windows
             // [G0, G0 + NWc): the 8 event classes its read has in each (zero outside the read)
@@ -823,10 +750,10 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 interior();
             }
         }
-        pf_ok = pf_early;
+        pf_ok = false;
         if (!kPfOn) {
             fetch_fields(chunk + (IT)gridDim.x);  // in flight during the walk
-        } else if (!pf2 && chunk + (IT)gridDim.x < n_chunks) {
+        } else if (chunk + (IT)gridDim.x < n_chunks) {
             const IT nb0 = (chunk + (IT)gridDim.x) * CR;
             const int nn = (int)(n_reads - nb0 < CR ? n_reads - nb0 : CR);
             const bool nv = tid < nn;
@@ -1152,17 +1079,6 @@ hipError_t launch_rc(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, 
     A.sums = A.runs && r.run_chunks == A.n_chunks ? A.runs + r.n_reads : nullptr;
     // resident blocks: LDS bounds a CU to 3 (event image + stage + histogram)
     const int64_t cap = 256 * 3;
-    if (!A.sums && kRcBalance) {
-        // Every resident block takes the same number of chunks: the reads are cut into rounds x
-        // cap chunks of at most nt reads (rounds = what nt-read chunks need), instead of full
-        // chunks and a last round that only some blocks take (1M reads: 3,907 chunks = 5 rounds of
-        // 768 + 67, whose latency chain the whole launch waits for).  The upload's chunk summaries
-        // describe nt-read chunks, so the indexed path keeps them.
-        const int64_t rounds = (A.n_chunks + cap - 1) / cap;
-        const int64_t per = (r.n_reads + rounds * cap - 1) / (rounds * cap);
-        A.chunk_reads = (int32_t)(per < nt ? (per > 64 ? per : 64) : nt);  // (at least a wave of reads)
-        A.n_chunks = (r.n_reads + A.chunk_reads - 1) / A.chunk_reads;
-    }
     const int64_t blocks = A.n_chunks < cap ? A.n_chunks : cap;
     const dim3 grid((unsigned)blocks), block(nt);
     A.trace = nullptr;

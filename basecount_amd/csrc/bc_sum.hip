@@ -21,8 +21,8 @@ namespace {
 //   k_sum_exact    one wave per listed leaf: its two tiles walked like k_pileup_solo, the leaf's
 //                  exact pairwise sum, coverage and non-zero count; first the tiles of the last
 //                  partial buffer, whose per-position coverage / entropy the fold's tail reads;
-//   k_sum_quarters numpy's pairwise tree over the 16 leaves of every 2048-position quarter
-//                  (the quarter partials the fold joins), re-zeroing the leaf arrays.
+//   k_sum_buffers  numpy's pairwise tree over the 64 leaves of every whole 8192-position buffer
+//                  (the per-buffer partials the fold adds in order), re-zeroing the leaf arrays.
 // The same numbers as k_pileup_solo<STORE = false> bit for bit, with ~10x fewer tile walks at
 // C5's depth (every non-empty tile there, only the overlapping ones here).
 
@@ -211,17 +211,17 @@ __global__ __launch_bounds__(256, 4) void k_sum_exact(PileArgs A) {
     }
 }
 
-// numpy's pairwise tree over a quarter's 16 leaves (16 lanes per quarter, left + right), the
-// leaves of single-read coverage as 128 - counted positions; the leaf arrays are zeroed again
-// for the next launch.
-__global__ __launch_bounds__(256) void k_sum_quarters(PileArgs A) {
+// numpy's pairwise tree over the 64 leaves of every whole 8192-position buffer (one wave per
+// buffer, lane = leaf; left + right at every level: the quarters' 16-leaf trees, then
+// (q0 + q1) + (q2 + q3)), the leaves of single-read coverage as 128 - counted positions, into the
+// per-buffer partials the fold adds in order; the leaf arrays are zeroed again for the next launch.
+__global__ __launch_bounds__(256) void k_sum_buffers(PileArgs A) {
     const int lane = threadIdx.x & 63;
-    const int64_t q = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
-    const int64_t nq = A.full_chunks * 4;
+    const int64_t buf = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     double v = 0.0;
     long long cs = 0, nz = 0;
-    if (q < nq) {
-        const int64_t l = q * 16 + (lane & 15);
+    if (buf < A.full_chunks) {
+        const int64_t l = buf * 64 + lane;
         const int32_t c = A.leaf_cnt[l], m = A.leaf_mark[l];
         if (m) {
             v = A.dval[m - 1];
@@ -235,16 +235,16 @@ __global__ __launch_bounds__(256) void k_sum_quarters(PileArgs A) {
         if (c) A.leaf_cnt[l] = 0;
     }
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
+    for (int o = 1; o < 64; o <<= 1) {
         const double w = __shfl_down(v, o);
         if ((lane & (2 * o - 1)) == 0) v = v + w;
         cs += __shfl_xor(cs, o);
         nz += __shfl_xor(nz, o);
     }
-    if ((lane & 15) == 0 && q < nq) {
-        A.sub_ent[q] = v;
-        A.sub_cov[q] = cs;
-        A.sub_nz[q] = nz;
+    if (lane == 0 && buf < A.full_chunks) {
+        A.sub_ent[buf] = v;
+        A.sub_cov[buf] = cs;
+        A.sub_nz[buf] = nz;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *A.ndirty = 0;  // k_sum_exact of this launch is done
 }
@@ -278,9 +278,10 @@ hipError_t launch_sum_sparse(hipStream_t s, const bc_reads& r, int64_t L, uint32
     A.dlist = A.leaf_mark + cap;
     A.dval = (double*)(A.dlist + cap);  // (cap even: 8-byte aligned)
     A.dcov = (long long*)(A.dval + cap);
-    A.sub_ent = parts.sub_ent;
-    A.sub_cov = parts.sub_cov;
-    A.sub_nz = parts.sub_nz;
+    A.sub_ent = parts.ent;  // (k_sum_buffers: whole-buffer partials)
+    A.sub_cov = parts.cov;
+    A.sub_nz = parts.nz;
+    parts.whole_buffers = true;
     A.cov_tail = parts.cov_tail;
     A.ent_tail = parts.ent_tail;
     A.n_tail_tiles = (L - A.full_chunks * kNpBuf + kTile - 1) / kTile;
@@ -290,12 +291,12 @@ hipError_t launch_sum_sparse(hipStream_t s, const bc_reads& r, int64_t L, uint32
     const size_t lds = (size_t)nw * (kRecBytes + kStageRegion + kSumTr * 8);
     int64_t xb = (A.n_tail_tiles + A.nleaf + nw - 1) / nw;
     xb = xb < 1024 ? (xb < 1 ? 1 : xb) : 1024;
-    const unsigned rb = (unsigned)((A.n + 255) / 256), qb = (unsigned)((A.full_chunks * 4 + 15) / 16);
+    const unsigned rb = (unsigned)((A.n + 255) / 256), qb = (unsigned)((A.full_chunks + 3) / 4);
 #define BC_SUMS(Q, KK)                                                                                   \
     do {                                                                                                 \
         if (rb) hipLaunchKernelGGL((k_sum_reads<Q, KK>), dim3(rb), dim3(256), 0, s, A);                 \
         hipLaunchKernelGGL((k_sum_exact<Q, KK>), dim3((unsigned)xb), dim3(64 * nw), lds, s, A);          \
-        if (qb) hipLaunchKernelGGL(k_sum_quarters, dim3(qb), dim3(256), 0, s, A);                       \
+        if (qb) hipLaunchKernelGGL(k_sum_buffers, dim3(qb), dim3(256), 0, s, A);                        \
     } while (0)
     if (mbq > 0) {
         if (k == 5) BC_SUMS(true, 5); else BC_SUMS(true, 6);

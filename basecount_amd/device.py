@@ -67,6 +67,7 @@ def lib() -> C.CDLL:
         "bc_device_count": ([C.POINTER(C.c_int)], C.c_int),
         "bc_ctx_create": ([C.c_int, vp, C.POINTER(vp)], C.c_int),
         "bc_ctx_destroy": ([vp], C.c_int),
+        "bc_ctx_release_scratch": ([vp], C.c_int),
         "bc_ctx_stream": ([vp, C.POINTER(vp)], C.c_int),
         "bc_sync": ([vp], C.c_int),
         "bc_ctx_set_shape": ([vp, C.c_int, C.c_int, C.c_int], C.c_int),
@@ -251,6 +252,10 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def release_scratch(self) -> None:
+        """bc_ctx_release_scratch: the context's own grow-only device scratch given back."""
+        check(lib().bc_ctx_release_scratch(self.h))
 
     def set_shape(self, shape: str = "auto", tile_waves: int = 0, reads_per_block: int = 0) -> None:
         """Kernel-shape override for bc_count / bc_pileup (bc_ctx_set_shape): "auto", "tile",

@@ -243,12 +243,25 @@ def _scratch(ctx) -> _Scratch:
     return sc
 
 
-def release_device_memory() -> None:
+# devices whose scratch a call with _keep_scratch=True asked to keep: a later call without the
+# flag leaves it in place, release_device_memory() frees it
+_KEPT: set = set()
+
+
+def release_device_memory(only_unkept: bool = False) -> None:
     """Free the HBM kept for reuse by the CLI and by library calls made with _keep_scratch
-    (batch buffers, outputs); get_basecounts / BaseCount release their own when they return."""
-    for sc in _SCRATCHES.values():
-        sc.release()
-    _SCRATCHES.clear()
+    (batch buffers, outputs, and the contexts' own kernel scratch: bc_ctx_release_scratch);
+    get_basecounts / BaseCount release what they used when they return (only_unkept: scratch
+    some earlier call asked to keep stays)."""
+    for dev in list(_SCRATCHES):
+        if only_unkept and dev in _KEPT:
+            continue
+        _SCRATCHES.pop(dev).release()
+    for dev, ctx in _CONTEXTS.items():
+        if not (only_unkept and dev in _KEPT):
+            ctx.release_scratch()
+    if not only_unkept:
+        _KEPT.clear()
 
 
 def _download(outs, counts, k, L) -> RefData:
@@ -543,8 +556,10 @@ def get_basecounts(bam, references=None, min_base_quality=0, min_mapping_quality
         return _get_basecounts_top(bam, references, min_base_quality, min_mapping_quality, chunk_size,
                                    show_n_bases, long_format, device, _mode, _tiles, _group)
     finally:
-        if _DEFERRED is None and not _keep_scratch:
-            release_device_memory()
+        if _keep_scratch:
+            _KEPT.update(_SCRATCHES)
+        elif _DEFERRED is None:
+            release_device_memory(only_unkept=True)
 
 
 def _get_basecounts_top(bam, references, min_base_quality, min_mapping_quality, chunk_size, show_n_bases,
@@ -892,17 +907,13 @@ def _no_reads() -> D.BcReads:
 
 def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
     """The slice as the fast kernels take it: an unsorted slice is first put in start order on
-    the device (bc_reads_sort, into the reusable scratch), then the tiled kernel's tile index
-    (bc_reads_index), stream-ordered before the kernels."""
+    the device (bc_reads_sort, into the reusable scratch).  No device index is built: a batch the
+    CLI counts once never recovers it (bench.py, driver-clock figures: C3's run records cost
+    k_index_runs ~19 us against ~12 us saved in k_rc; C2's tile index k_index_tiles ~6 us
+    against ~0.8 us saved in k_pileup, whose tile groups then search pos[] themselves)."""
     if not reads.sorted and reads.n_reads > 1:
         nb = ctx.sort_bytes(reads)
         reads = ctx.sort(reads, scratch.get("sorted", nb).ptr, nb)
-    # the tile index only: a batch counted once does not recover the run records' build (C3:
-    # k_index_runs ~18 us against ~10 us saved in k_rc; bench.py reports both), and none for a
-    # slice the read-chunked kernel takes (what BC_INDEX_AUTO would build is not the tiles)
-    nb = ctx.index_bytes(reads, L, D.BC_INDEX_TILES)
-    if nb and ctx.index_bytes(reads, L, D.BC_INDEX_AUTO) == nb:
-        ctx.index(reads, L, scratch.get("index", nb).ptr, nb, D.BC_INDEX_TILES)
     return reads
 
 

@@ -4,22 +4,26 @@ A step = one pass of the hot path over one batch already resident in HBM: kernel
 + base counting, count.cpp:22-97) and kernel 2 (per-position coverage / percentages /
 entropies, main.py:29-78), for every contig the rank owns.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5] [--launch graph|eager]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--launch graph|eager]
 
-Headline (``value``): BASELINE config 2 (1 contig 29,903 bp, 100,000 reads x 150 bp, all-M CIGAR),
-one launch of the fused k_pileup per step, the K timed steps replayed from one hipGraph
-(``--launch eager`` issues them one by one).  At N>1 every rank runs its own contig of that
-shape (contigs are independent: weak scaling, no collective inside the step); the per-contig
-summaries are gathered to rank 0 over RCCL once after the timed region (``gather_ms``).
+Headline (``value``), as BASELINE.json quotes its configs:
+  * one GPU: config 2 (1 contig 29,903 bp, 100,000 reads x 150 bp, all-M CIGAR), one launch of
+    the fused k_pileup per step, the K timed steps replayed from one hipGraph (``--launch eager``
+    issues them one by one);
+  * N > 1 GPUs: config 5, the 8-GPU config (24 GRCh38-sized contigs, 3.09 Gb, 50,000 reads each)
+    sharded over the ranks (LPT on length, strong scaling: every step is the whole job), as
+    ``--summarise`` runs it (main.py:469-499: the read-parallel summary, bc_sum.hip, and one fold
+    per rank), each step ending with the RCCL gather of every contig's summary to rank 0.
 
 ``extra`` carries the other BASELINE shapes, each timed the same way with its own roofline:
-  * c3 (N=1): 1,000,000 mixed-CIGAR reads on the same contig (deep: k_rc + k_stats);
-  * c5 (every N): 24 GRCh38-sized contigs (3.09 Gb) x 50,000 reads, sharded over the ranks (LPT,
-    strong scaling), summary-shaped (main.py:469-499: no per-position percentages; every
-    per-position count, coverage and entropy is still written), bc_pileup_partials per contig
-    (the sparse sweep also computes numpy's buffer partial sums) and one bc_summary_fold for all
-    of the rank's contigs, each step ending with the RCCL gather of every contig's summary to
-    rank 0 (``gather_us``).
+  * c3 (N=1): 1,000,000 mixed-CIGAR reads on the same contig (deep: k_rc + k_stats), also at
+    --min-base-quality 20 (c3_q20) and in random order (c3_unsorted);
+  * c4 (N=1): c3 + the 98-amplicon BED (--summarise-with-bed: + summary and k_amplicon);
+  * c5 (N=1): as the headline at N > 1, with the storing variant (every per-position count,
+    coverage and entropy written) beside it;
+  * c2 (N>1): every rank its own contig of C2's shape (weak scaling), the per-contig summaries
+    gathered to rank 0 after the timed region (``gather_ms``); c3_split: C3's contig split over
+    the ranks by read, histograms reduced to rank 0 over RCCL.
 At N=1 rank 0 also times the reference's CPU path (its own compiled count.cpp + get_stats, one
 core), the all-cores C restatement (``cpu_baseline_all_cores``), and the CLI end to end on the C2
 BAM (decode, upload, kernels, formatting: ``e2e``).
@@ -634,6 +638,26 @@ def gather_summaries(group, wl) -> tuple:
     return sizes, dst
 
 
+def gather_rows_summaries(ctx, group, wl, rank: int, world: int) -> float:
+    """After a weak-scaling run (each rank its own contig): every contig's summary (bc_summary on
+    the step's outputs) gathered to rank 0 over the group, the gather timed (ms, max over ranks)."""
+    from basecount_amd import device as D
+
+    payload = []
+    for _, L, _, _, o in wl.work:
+        work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        ctx.summary(o["cov"].ptr, o["ent"].ptr, L, work.ptr, dout.ptr)
+        payload.append(dout.download(np.float64, 4))
+    data = np.concatenate(payload).tobytes()
+    group.barrier()
+    g0 = time.perf_counter()
+    parts = group.gather_bytes(data)
+    ms = max_over_ranks(group, time.perf_counter() - g0) * 1e3
+    if rank == 0:
+        assert len(parts) == world and parts[0] == data
+    return ms
+
+
 def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, warmup: int,
                launch: str, summarise: bool, summary_only: bool = False) -> dict:
     """Time K steps of one config (the bench contract: W warmup, barrier + sync on both sides,
@@ -1235,7 +1259,9 @@ def main():
                     help="start the ranks and join their process group only (no GPU work)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--config", default=None, choices=sorted(WORKLOADS),
+                    help="headline workload (default: c2 on one GPU; c5, BASELINE's multi-GPU config, sharded "
+                         "over the ranks with the RCCL gather, on several)")
     ap.add_argument("--mbq", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -1271,6 +1297,8 @@ def main():
 
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
+    if args.config is None:  # BASELINE: C2 is the one-GPU config, C5 (24 contigs) the 8-GPU one
+        args.config = "c2" if args.gpus == 1 else "c5"
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: this process starts the N ranks itself (before anything touches the GPU)
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
@@ -1321,24 +1349,15 @@ def main():
     # ---- gather of the per-contig summaries to rank 0 (the output step, after the timed region)
     gather_ms = None
     if group is not None and args.config not in ("c4", "c5"):
-        payload = []
-        for _, L, _, _, o in wl.work:
-            work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
-            ctx.summary(o["cov"].ptr, o["ent"].ptr, L, work.ptr, dout.ptr)
-            payload.append(dout.download(np.float64, 4))
-        data = np.concatenate(payload).tobytes()
-        group.barrier()
-        g0 = time.perf_counter()
-        parts = group.gather_bytes(data)
-        gather_ms = max_over_ranks(group, time.perf_counter() - g0) * 1e3
-        if rank == 0:
-            assert len(parts) == world and parts[0] == data
+        gather_ms = gather_rows_summaries(ctx, group, wl, rank, world)
     wl.free()
     del wl
 
     extra = {}
     if not args.no_extras:
-        todo = (["c3", "c4", "c5"] if world == 1 else ["c5"])
+        # one GPU: the other single-GPU configs and C5; several: C5 is the headline (strong scaling,
+        # sharded + gathered) and C2 weak scaling (each rank its own contig) rides along
+        todo = (["c3", "c4", "c5"] if world == 1 else ["c2", "c5"])
         for cfg in todo:
             if cfg == args.config:
                 continue
@@ -1347,6 +1366,13 @@ def main():
                 r = run_c5(ctx, group, args, rank, world, st, wu, args.launch)
             elif cfg == "c4":  # --summarise-with-bed: kernels 1 + 2, summary and amplicons per step
                 r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=True)
+            elif cfg == "c2" and world > 1:  # weak scaling, the per-contig summaries gathered after
+                r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=False)
+                w2 = r.pop("_wl")
+                r["gather_ms"] = gather_rows_summaries(ctx, group, w2, rank, world)
+                w2.free()
+                extra[cfg] = r
+                continue
             else:
                 r = run_config(cfg, ctx, group, args, rank, world, st, wu, args.launch, summarise=False)
             r.pop("_wl").free()
@@ -1417,7 +1443,7 @@ def main():
             "config": {"workload": head["workload"], "reads_per_rank": head["reads_per_rank"],
                        "positions_per_rank": head["positions_per_rank"],
                        "contigs_per_rank": head["contigs_per_rank"], "min_base_quality": args.mbq,
-                       "percentages_stored": args.config != "c5",
+                       "percentages_stored": args.config in ("c2", "c3"),
                        "parallelism": f"contig-sharded x{world}"
                                       + (f" over {group.backend}" if group is not None else ""),
                        "comm": (group.backend if group is not None else None),
@@ -1440,6 +1466,7 @@ def main():
         }
         if "gather_us" in head:
             line["gather_us"] = head["gather_us"]
+            line["gather_bytes"] = head.get("gather_bytes")
         line["steps_in_flight"] = head["steps_in_flight"]
         line["launch_trial"] = head.get("launch_trial")
         if "serial_us_per_step" in head:

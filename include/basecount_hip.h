@@ -125,6 +125,11 @@ int bc_device_count(int* n);
 int bc_ctx_create(int device, void* stream, bc_ctx** out);
 int bc_ctx_destroy(bc_ctx* ctx);
 int bc_ctx_stream(bc_ctx* ctx, void** stream);
+/* Give back the context's grow-only device scratch (bc_pileup's k_rc accumulation buffer,
+ * bc_pileup_partials' stand-in outputs and the read-parallel summary's leaf arrays) after
+ * finishing the work enqueued on its stream; the next call that needs one allocates it again
+ * (outside any graph capture).  The context stays usable.                                      */
+int bc_ctx_release_scratch(bc_ctx* ctx);
 
 /* Kernel-shape selection for bc_count / bc_pileup on this context (parity tests and tuning; no
  * shape skips work, every one computes the same counts).  The default, BC_SHAPE_AUTO, picks

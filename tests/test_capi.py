@@ -53,4 +53,5 @@ def test_hip_library_rejects_null_arguments_without_touching_a_device():
     assert b"NULL" in L.bc_last_error()
     assert L.bc_sync(None) == D.BC_E_ARG
     assert L.bc_ctx_set_shape(None, 0, 0, 0) == D.BC_E_ARG
+    assert L.bc_ctx_release_scratch(None) == D.BC_E_ARG
     assert L.bc_pileup(None, None, 0, 0, 5, 0.0, 0.0, None, None, None, None, None) == D.BC_E_ARG

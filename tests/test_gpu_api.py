@@ -61,3 +61,25 @@ def test_api_matches_reference(ours, case):
         gold = json.loads(fh.read())
     d = _diff(ours[case], gold)
     assert d is None, f"{case}: {d}"
+
+
+@pytest.mark.gpu
+def test_release_keeps_another_callers_scratch():
+    """a get_basecounts call without _keep_scratch releases only scratch nobody asked
+    to keep; release_device_memory() then gives back everything, the contexts' own kernel scratch
+    (bc_ctx_release_scratch) included, and later calls still work."""
+    sys.path.insert(0, REPO)
+    from basecount_amd import main as M
+
+    bam = os.path.join(GOLD, "mixed.bam")
+    a = M.get_basecounts(bam, _mode="summary", _keep_scratch=True)
+    kept = set(M._SCRATCHES)
+    assert kept and kept <= M._KEPT
+    b = M.get_basecounts(bam, _mode="summary")
+    assert set(M._SCRATCHES) == kept  # the kept cache survived the plain call
+    M.release_device_memory()
+    assert not M._SCRATCHES and not M._KEPT
+    c = M.get_basecounts(bam, _mode="summary")
+    assert not M._SCRATCHES  # a plain call releases its own scratch
+    for ref in a:
+        assert a[ref]["summary"]["avg_cov"] == b[ref]["summary"]["avg_cov"] == c[ref]["summary"]["avg_cov"]

@@ -117,8 +117,9 @@ def test_cli_rccl_world1_matches_golden(tmp_path):
 def test_bench_gpus_2_rehearsal():
     """`bench.py --gpus 2` as the driver runs it (no launcher: the script starts its two ranks),
     both ranks on the box's one GPU with the exchange over gloo (RCCL refuses two ranks on one
-    GPU): one JSON line from rank 0 with n_gpus 2, the C5 strong-scaling extra gathered from
-    both ranks, parity true."""
+    GPU): one JSON line from rank 0 with n_gpus 2 whose headline is C5 (strong scaling, every
+    contig's summary gathered from both ranks), C2 weak scaling and C3 split as extras, parity
+    true."""
     env = dict(os.environ, BASECOUNT_DIST_BACKEND="gloo")
     for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(v, None)
@@ -129,8 +130,10 @@ def test_bench_gpus_2_rehearsal():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["comm"] == "gloo" and d["parity_vs_oracle"]
-    c5 = d["extra"]["c5"]
-    assert c5["parity_vs_oracle"] and c5["gather_bytes"] == 32 * 24 and c5["scaling"] == "strong"
+    assert d["scaling"] == "strong" and d["gather_bytes"] == 32 * 24 and d["config"]["contigs_per_rank"] >= 1
+    assert d["config"]["workload"].startswith("C5") and "c5" not in d["extra"]
+    c2 = d["extra"]["c2"]  # every rank its own C2-shaped contig
+    assert c2["parity_vs_oracle"] and c2["scaling"] == "weak" and c2["gather_ms"] is not None
     sp = d["extra"]["c3_split"]  # C3's one contig split over the two ranks, histograms reduced
     assert sp["parity_vs_oracle"] and sp["reads_per_rank"] == 500_000 and sp["scaling"] == "strong"
 

@@ -134,7 +134,7 @@ def shaped_batch(rng, L, n, templates, nfrac=0.02):
         codes[rng.random(q) < nfrac] = rng.choice([15, 0, 5, 3])
         seqs.append(codes)
         quals.append(rng.integers(0, 45, q).astype(np.uint8))
-        pos.append(int(rng.integers(0, L - span)) if starts is None else int(starts(rng, span)))
+        pos.append(int(rng.integers(0, L - span)))
         cigs.append(ops)
     order = np.argsort(pos, kind="stable")
     pos, cigs = [pos[i] for i in order], [cigs[i] for i in order]
@@ -877,6 +877,41 @@ def test_rc_64bit_indices_chromosome_scale(ctx, mbq, ncols):
     assert br2 >= 0
     _, bad2 = gpu_count(ctx, b, L2, mbq, ncols)
     assert bad2 == br2
+
+
+@pytest.mark.parametrize("mbq,k", [(0, 5), (20, 6)])
+def test_rc_pileup_64bit_chromosome_scale(ctx, mbq, k):
+    """the pileup chain at chromosome scale (int64_t k_rc + k_stats_lane,
+    L = 2^27 + 10,000) against the oracle on both 20,000-position windows: counts, coverage,
+    percentages and both entropies (bit-identical; the 1e-6 bound asserted too)."""
+    ctx.set_shape("rc")
+    L = (1 << 27) + 10_000
+    rng = np.random.default_rng(91 + mbq)
+    b = shaped_batch(rng, 20_000, 20_000, IMAGE_DEEP + FALLBACK)
+    far = np.arange(b["pos"].size) >= 40
+    b["pos"] = (b["pos"].astype(np.int64) + np.where(far, L - 20_000, 0)).astype(np.int32)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    nf, nf2 = norm_factors(k)
+    r = D.DeviceReads(ctx, b)
+    bufs = [ctx.alloc(x) for x in (4 * k * L, 4 * L, 8 * k * L, 8 * L, 8 * L)]
+    ctx.pileup(r, L, mbq, k, nf, nf2, *(x.ptr for x in bufs))
+    assert ctx.range_error() == -1
+    for lo, hi in ((0, 20_000), (L - 20_000, L)):
+        n = hi - lo
+        cov_o, pc_o, ent_o, sec_o = O.stats(exp[lo:hi], k == 6)
+        for c in range(k):
+            got = bufs[0].download(np.int32, n, offset_bytes=4 * (c * L + lo))
+            assert np.array_equal(got, exp[lo:hi, c].astype(np.int32)), (lo, c)
+            gpc = bufs[2].download(np.float64, n, offset_bytes=8 * (c * L + lo))
+            assert np.array_equal(gpc, pc_o[c]), (lo, c)
+        assert np.array_equal(bufs[1].download(np.int32, n, offset_bytes=4 * lo), cov_o)
+        ent, sec = bufs[3].download(np.float64, n, offset_bytes=8 * lo), bufs[4].download(np.float64, n, offset_bytes=8 * lo)
+        assert np.max(np.abs(ent - ent_o)) <= 1e-6 and np.max(np.abs(sec - sec_o)) <= 1e-6
+        assert np.array_equal(ent, ent_o) and np.array_equal(sec, sec_o)
+    for x in bufs:
+        x.free()
+    r.free()
 
 
 @pytest.mark.parametrize("L,n,mbq,show_n", [

@@ -1,12 +1,13 @@
 #!/bin/bash
 # The round's profiles in one GPU session: rocprofv3 kernel traces (--kernel-trace --stats) of
-# the bench for c2 / c3 / c5, then separate PMC passes (HBM bytes: FETCH_SIZE, WRITE_SIZE; and the
-# instruction counters for c2 / c3).  Stops at the first fault / abort / timeout.
+# the bench per config (CFGS, default c2 c3 c3q20 c4 c5), then separate PMC passes (instruction and
+# wait counters, LDS, HBM bytes: FETCH_SIZE, WRITE_SIZE) for every config.  Stops at the first
+# fault / abort / timeout.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-for c in ${CFGS:-c2 c3 c5 c3q20}; do
+for c in ${CFGS:-c2 c3 c3q20 c4 c5}; do
   steps=200; extra=""; cfg=$c
   [ "$c" = c5 ] && steps=5 && extra="--streams 1"  # c5: launches serialized, so their durations add up
   [ "$c" = c3q20 ] && cfg=c3 && extra="--mbq 20"   # C3 with the quality test (QUAL bytes read)
@@ -14,8 +15,8 @@ for c in ${CFGS:-c2 c3 c5 c3q20}; do
     python bench.py --config $cfg --no-cpu-baseline --no-extras --no-e2e --lean --launch eager --steps $steps --warmup 2 $extra \
     > gpurun_out/prof_$c.log 2>&1
   rc=$?; echo "trace $c rc=$rc"; fatal $rc && exit $rc
-  passes="4 5"; [ "$c" = c2 ] || [ "$c" = c3 ] && passes="1 2 3 4 5"
-  PASSES="$passes" BENCH_ARGS="--config $cfg $([ "$c" = c3q20 ] && echo --mbq 20)" OUT=pmc_$c bash scripts/pmc.sh
+  pargs="--config $cfg"; [ "$c" = c3q20 ] && pargs="$pargs --mbq 20"; [ "$c" = c5 ] && pargs="$pargs --steps 5 --streams 1"
+  PASSES="${PASSES:-1 2 3 4 5}" BENCH_ARGS="$pargs" OUT=pmc_$c bash scripts/pmc.sh
   rc=$?; fatal $rc && exit $rc
 done
 echo PROFILES_DONE

@@ -3,7 +3,8 @@ kernel's counters averaged over its dispatches, and the HBM bytes per launch com
 MI355X_MICROARCH.md prescribes for gfx950: (2 x FETCH_SIZE + WRITE_SIZE) KiB.
 
     python scripts/pmc_json.py profiles/r03_pmc.json profiles/kernel1_pmc.json \\
-        c2=gpurun_out/pmc_c2:k_pileup:pileup:1 c3=gpurun_out/pmc_c3:k_rc:rc:3 c5=gpurun_out/pmc_c5:k_pileup_solo:solo:1:24
+        c2=gpurun_out/pmc_c2:k_pileup:pileup:1 c3=gpurun_out/pmc_c3:k_rc:rc:3 \\
+        c5=gpurun_out/pmc_c5:k_sum_reads+k_sum_exact+k_sum_buffers:solo_sum:1:24
 
 Each spec is dir:kernel-name-substring:bench-kernel-key:batch-copies[:launches-per-step[:mbq]]
 (name c3_q20 for the C3 run at --mbq 20: bench.py looks entries up as <config>[_q<mbq>]).  The
@@ -22,6 +23,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def summarise(d, pat):
+    """Per-dispatch averages of the kernels matching pat; "a+b+c" sums the averages of a, b and
+    c (kernels that run once each per launch of the step's unit, e.g. C5's three summary kernels
+    per contig)."""
+    if "+" in pat:
+        parts = [summarise(d, p) for p in pat.split("+")]
+        out = {}
+        for k in parts[0]:
+            if k != "dispatches" and all(k in q for q in parts):
+                out[k] = sum(q[k] for q in parts)
+        out["dispatches"] = min(q["dispatches"] for q in parts)
+        return out
     agg = collections.defaultdict(list)
     for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):

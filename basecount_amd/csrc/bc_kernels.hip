@@ -709,22 +709,18 @@ __global__ __launch_bounds__(256) void k_sum_tail(const int32_t* cov, const doub
     }
 }
 
-// The float64 fold over the per-buffer partials: numpy adds the buffers' pairwise sums in order,
-// s_j = fl(s_{j-1} + b_j), one rounding per buffer.  The fold reproduces that sequence exactly
-// without one dependent add per buffer.  The partials are >= 0, so s only grows; while s stays in
-// one binade [2^e, 2^(e+1)) every s_j is a multiple of u = ulp(s) = 2^(e-52), and
-//   fl(s_{j-1} + b_j) = s_{j-1} + rint(b_j / u) * u
-// exactly, unless b_j / u is a tie (fraction exactly 1/2: round-half-even then depends on the
-// parity of s_{j-1} / u) or the sum reaches 2^(e+1) (the grid coarsens).  So s / u is an integer
-// A < 2^53 and the buffers up to the first one that breaks either condition add as integers:
-// r_j = rint(b_j / u) (exact: b_j * 2^(52-e) is exact), one block-wide scan of the r_j finds the
-// first j whose running total reaches 2^53 - A or whose r_j is a tie, the buffers before it are
-// added at once (A + their total < 2^53: one exact add), and buffer j itself with one fp64 add,
-// as numpy does; then the next binade.  Steps per reference: its rounds (4096 buffers each) plus
-// the binades s crosses (~15 for a chromosome) plus the ties (none seen): a few dozen block scans
-// instead of ~30,000 dependent adds.  The integer coverage / non-zero sums reduce in parallel.
-// One workgroup per reference; the partials are double-buffered through LDS (round r+1 loads in
-// flight while round r is folded).
+// The float64 fold over the per-buffer partials stays sequential (numpy adds the buffers'
+// pairwise sums in order), but it need not take one dependent add per buffer.  Buffer sums are
+// >= 0, and most are integers (8192 positions whose entropies are 0.0 / 1.0: every buffer no two
+// reads share a position of; exactly 8192.0 without reads).  Adding integers to s rounds only
+// where s crosses into a binade whose ulp exceeds the granularity of its fraction, and then the
+// final sum of the run is not representable either: so a run of integer buffers adds as ONE add
+// of its exact integer total whenever that add is exact (TwoSum error 0), and only fractional
+// buffers (and the rare run that crosses such a binade) take sequential adds.  One workgroup per
+// reference, so the folds of several references (bc_summary_fold) run side by side.  The
+// partials are double-buffered through LDS, 1024 per round: the block loads round r+1 into
+// registers while round r is scanned (the integer buffers' exact prefix sums and the list of the
+// fractional ones) and folded by thread 0 from LDS.  The integer sums reduce in parallel.
 struct FoldRef {
     const double* pe;
     const long long* pc;
@@ -744,14 +740,20 @@ struct FoldArgs {
 
 constexpr int kFoldThreads = 1024;
 __global__ __launch_bounds__(kFoldThreads) void k_sum_final(FoldArgs FA) {
-    constexpr int kR = 4 * kFoldThreads;  // buffers per round, 4 per thread (thread t: 4t .. 4t+3)
+    constexpr int kR = 4 * kFoldThreads;  // buffers per round, 4 per thread
     constexpr int kW = kFoldThreads / 64;
     __shared__ double s_buf[kR];
-    __shared__ long long s_wtot[kW];
-    __shared__ int s_wbrk[kW];
-    __shared__ long long s_bulk;
-    __shared__ double s_s;
-    __shared__ int s_pos;
+    // The walk (rounds with at most kE fractional buffers): per fractional buffer, in order, its
+    // index, the exclusive prefix of the round's integer buffer sums (<= 8192 each) before it, its
+    // value, and the running sum s before its run (the optimistic chain's record)
+    constexpr int kE = kR / 4;
+    constexpr int kB = 8;  // events per batch of the chain
+    __shared__ uint16_t s_fr[kE];
+    __shared__ int s_fpre[kE + 1 + kB];   // (past the last event: the round's total, repeated)
+    __shared__ double s_fv[kE + 1 + kB];  // (past the last fractional buffer: 0.0)
+    __shared__ double s_rd[kE + 1 + kB];  // each event's integer run total, as a double (exact)
+    __shared__ int s_total;  // the round's integer buffer sum
+    __shared__ int s_wsum[kW], s_wfr[kW];
     __shared__ long long s_red[2 * kW];
     const FoldRef& R = FA.ref[blockIdx.x];
     const double* part_ent = R.pe;
@@ -760,13 +762,14 @@ __global__ __launch_bounds__(kFoldThreads) void k_sum_final(FoldArgs FA) {
     const int64_t nchunks = R.nchunks;
     const int64_t nq = *R.nquart;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    double s = 0.0;
     long long cs = 0, nz = 0;
     double v[4];
     long long vc[4], vn[4];
     auto load = [&](int64_t r0) {  // issue only: the values are consumed a round later
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int64_t c = r0 + 4 * t + j;
+            const int64_t c = r0 + t + kFoldThreads * j;
             if (c < nq) {  // a buffer's 4 quarters: (q0 + q1) + (q2 + q3), numpy's tree
                 const double* q = R.qe + 4 * c;
                 v[j] = (q[0] + q[1]) + (q[2] + q[3]);
@@ -783,107 +786,137 @@ __global__ __launch_bounds__(kFoldThreads) void k_sum_final(FoldArgs FA) {
     auto stash = [&]() {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            s_buf[4 * t + j] = v[j];
+            s_buf[t + kFoldThreads * j] = v[j];
             cs += vc[j];
             nz += vn[j];
         }
     };
-    constexpr long long kTwo53 = 1ll << 53;
-    // fold buffers [0, m) of the round into s_s
-    auto fold_round = [&](int m) {
-        for (;;) {
-            const int pos = s_pos;  // (uniform; written by thread 0 before a barrier)
-            if (pos >= m) break;
-            const double sv = s_s;
-            if (sv == 0.0) {  // the first buffer: 0.0 + b = b exactly
-                __syncthreads();
-                if (t == 0) {
-                    s_s = s_buf[pos];
-                    s_pos = pos + 1;
-                }
-                __syncthreads();
-                continue;
-            }
-            const int e = (int)(((unsigned long long)__double_as_longlong(sv) >> 52) & 0x7FF) - 1023;
-            const long long A = (long long)__builtin_ldexp(sv, 52 - e);  // s / ulp(s), in [2^52, 2^53)
-            const long long lim = kTwo53 - A;
-            long long r[4];
-            bool brk[4];
-            long long tot = 0;
+    // the round's scan: thread t takes buffers 4t .. 4t+3 (in order); integer sums as int (a
+    // round's total <= 4096 * 8192), fractional buffers listed in order
+    auto scan = [&](int m) {
+        int isum = 0, nfr = 0, iv[4];
+        bool fr[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int idx = 4 * t + j;
-                const bool in = idx >= pos && idx < m;
-                const double x = in ? __builtin_ldexp(s_buf[idx], 52 - e) : 0.0;  // b / u, exact
-                const bool big = x >= 9007199254740992.0;                          // >= 2^53
-                const double fl = __builtin_floor(x), f = x - fl;                  // (exact below 2^53)
-                r[j] = big ? kTwo53 : (long long)fl + (f > 0.5 ? 1 : 0);
-                brk[j] = in && !big && f == 0.5;  // a tie: the sum's parity decides
-                tot += r[j];
-            }
-            // inclusive scan of the thread totals (element order = thread order)
-            long long inc = tot;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const long long y = __shfl_up(inc, o);
-                if (lane >= o) inc += y;
-            }
-            if (lane == 63) s_wtot[wave] = inc;
-            __syncthreads();
-            long long before = 0;
-            for (int w = 0; w < wave; ++w) before += s_wtot[w];
-            // the first buffer that breaks the run: its running total reaches lim, or a tie
-            long long run = before + inc - tot;  // exclusive prefix of this thread's first buffer
-            int first = m;
-            long long bulk_here = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int idx = 4 * t + j;
-                const bool in = idx >= pos && idx < m;
-                if (in && first == m && (brk[j] || run + r[j] >= lim)) {
-                    first = idx;
-                    bulk_here = run;
-                }
-                run += r[j];
-            }
-            int fw = first;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const int y = __shfl_xor(fw, o);
-                fw = y < fw ? y : fw;
-            }
-            if (lane == 0) s_wbrk[wave] = fw;
-            __syncthreads();
-            int k = m;
-            for (int w = 0; w < kW; ++w) k = s_wbrk[w] < k ? s_wbrk[w] : k;
-            if (k < m && first == k) s_bulk = bulk_here;  // the owner of buffer k
-            if (k == m && t == kFoldThreads - 1) s_bulk = run;  // no break: every buffer of the round
-            __syncthreads();
-            if (t == 0) {
-                const double u = __builtin_ldexp(1.0, e - 52);
-                double x = sv + (double)s_bulk * u;  // (A + bulk) * u < 2^(e+1): exact
-                if (k < m) x = x + s_buf[k];        // the breaking buffer: numpy's own rounding
-                s_s = x;
-                s_pos = k < m ? k + 1 : m;
-            }
-            __syncthreads();
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * t + j;
+            const double x = e < m ? s_buf[e] : 0.0;
+            fr[j] = e < m && x != __builtin_floor(x);
+            iv[j] = fr[j] ? 0 : (int)x;
+            isum += iv[j];
+            nfr += fr[j] ? 1 : 0;
         }
+        int ps = isum, pf = nfr;  // inclusive wave scans
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int a = __shfl_up(ps, o), f = __shfl_up(pf, o);
+            if (lane >= o) ps += a, pf += f;
+        }
+        if (lane == 63) s_wsum[wave] = ps, s_wfr[wave] = pf;
+        __syncthreads();
+        int bs = 0, bf = 0, tf = 0;
+        for (int w = 0; w < kW; ++w) {
+            if (w < wave) bs += s_wsum[w], bf += s_wfr[w];
+            tf += s_wfr[w];
+        }
+        int xs = bs + ps - isum, xf = bf + pf - nfr;  // exclusive
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * t + j;
+            if (fr[j]) {
+                if (xf < kE) {
+                    s_fr[xf] = (uint16_t)e;
+                    s_fpre[xf] = xs;
+                    s_fv[xf] = s_buf[e];
+                }
+                ++xf;
+            }
+            xs += iv[j];
+        }
+        if (t == kFoldThreads - 1) s_total = xs;
+        __syncthreads();
+        return tf;
     };
-    if (t == 0) {
-        s_s = 0.0;
-        s_pos = 0;
-    }
     load(0);
     stash();
     __syncthreads();
     for (int64_t r0 = 0; r0 < nchunks; r0 += kR) {
         const bool more = r0 + kR < nchunks;
-        if (more) load(r0 + kR);  // in flight while this round is folded
+        if (more) load(r0 + kR);  // in flight while this round is scanned and folded
         const int m = (int)((nchunks - r0) < kR ? (nchunks - r0) : kR);
-        fold_round(m);
-        __syncthreads();  // s_buf read
+        const int nfr = scan(m);
+        const bool walk = nfr <= kE && 4 * nfr <= m;  // (uniform) few fractional buffers: the event walk
+        if (!walk) {
+            if (t == 0) {  // mostly fractional: plain sequential adds
+                const double* b = s_buf;
+                int i = 0;
+                for (; i + 8 <= m; i += 8) {
+                    double w[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) w[u] = b[i + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) s += w[u];
+                }
+                for (; i < m; ++i) s += b[i];
+            }
+        } else {
+            // Each fractional buffer f ends an integer run of exact total R_f (prefix difference;
+            // event nfr: the round's last run): s = (s + R_f) + v_f, two adds per event, by thread
+            // 0 alone.  The run's add (and every partial sum inside it, all smaller) is exact when
+            // s + R_f lies in the binade of s (multiples of ulp(s) <= 1): checked with integer ops
+            // on the exponent bits, off the add chain, per batch of kB events (loads of the next
+            // batch in flight); a batch with a run leaving its binade (a few per reference) is
+            // redone buffer by buffer from the s before it.
+            if (t <= kB) {  // the last run and the batch padding: x unchanged past it
+                s_fpre[nfr + t] = s_total;
+                s_fv[nfr + t] = 0.0;
+            }
+            __syncthreads();
+            for (int f = t; f <= nfr + kB; f += kFoldThreads)
+                s_rd[f] = (double)(s_fpre[f] - (f ? s_fpre[f - 1] : 0));
+            __syncthreads();
+            if (t == 0) {
+                auto hi = [](double v) { return (uint32_t)((unsigned long long)__double_as_longlong(v) >> 32); };
+                double x = s, rdA[kB], fvA[kB];
+#pragma unroll
+                for (int u = 0; u < kB; ++u) rdA[u] = s_rd[u], fvA[u] = s_fv[u];
+                for (int f0 = 0; f0 <= nfr; f0 += kB) {
+                    double rdB[kB], fvB[kB];
+                    const int fn = f0 + kB <= nfr ? f0 + kB : f0;  // (the next batch, or a reload)
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) rdB[u] = s_rd[fn + u], fvB[u] = s_fv[fn + u];
+                    const double x0 = x;
+                    uint32_t moved = 0;
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) {
+                        const double tt = x + rdA[u];
+                        moved |= (hi(x) ^ hi(tt)) & 0xFFF00000u;  // the exponent changed
+                        x = tt + fvA[u];  // (past the last event: + 0.0 + 0.0, exact)
+                    }
+                    // (a batch of integer buffers only, from an integer-valued s: exact below 2^53)
+                    if (moved && !(f0 == nfr && x0 == __builtin_floor(x0) && x < 9007199254740992.0)) {
+                        // redo the batch's buffers one by one, loaded 8 at a time
+                        const int last = f0 + kB - 1 < nfr ? f0 + kB - 1 : nfr;
+                        const int i0 = f0 == 0 ? 0 : (int)s_fr[f0 - 1] + 1;
+                        const int i1 = last < nfr ? (int)s_fr[last] + 1 : m;
+                        x = x0;
+                        int i = i0;
+                        for (; i + 8 <= i1; i += 8) {
+                            double w[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) w[u] = s_buf[i + u];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) x += w[u];
+                        }
+                        for (; i < i1; ++i) x += s_buf[i];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) rdA[u] = rdB[u], fvA[u] = fvB[u];
+                }
+                s = x;
+            }
+        }
+        __syncthreads();  // s_buf read by thread 0
         if (more) stash();
-        if (t == 0) s_pos = 0;
         __syncthreads();
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -901,7 +934,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_sum_final(FoldArgs FA) {
         for (int w = 0; w < kW; ++w) cs += s_red[w], nz += s_red[kW + w];
         const double n = (double)R.L;
         R.out[0] = (double)cs / n;  // integer sum is exact in float64 below 2^53: np.mean == sum / n
-        R.out[1] = s_s / n;
+        R.out[1] = s / n;
         R.out[2] = (double)nz;
         R.out[3] = (double)cs;
     }

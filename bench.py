@@ -69,8 +69,8 @@ KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "solo": "k_pileup_sol
                              "coverage, numpy mean and median of both entropies)",
                 "index": "k_index_runs + k_index_tiles (the batch's device index, bc_reads_index)",
                 "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)",
-                "solo_sum": "k_pileup_solo summary-only sweep (kernels 1 + 2 fused, numpy's partials, no per-position "
-                            "output)"}
+                "solo_sum": "summary-only kernels 1 + 2, read-parallel (k_sum_reads + k_sum_exact + k_sum_buffers per "
+                            "contig; durations summed over the contigs' launches, which overlap on the streams)"}
 
 
 def read_bytes(b: dict, mbq: int, l_seq: np.ndarray) -> int:
@@ -88,9 +88,10 @@ def kernel_bytes(kernel: str, rb: int, L: int, k: int, with_pc: bool = True) -> 
     entropies; k_rc reads the batch and writes the counts; k_stats reads the counts and writes
     the statistics."""
     stats_out = L * (4 + (8 * k if with_pc else 0) + 16)
-    # the summary-only sweep: the reads, 24 B of partials per 2048-position quarter and the last
-    # partial buffer's coverage + entropy (12 B per position)
-    sum_only = rb + 24 * (L // 2048) + 12 * (L % 8192)
+    # the read-parallel summary-only call (bc_sum.hip): the reads, the leaf arrays every whole
+    # buffer's leaves are read from (count + mark, 8 B per 128-position leaf), 24 B of partials per
+    # 8192-position buffer and the last partial buffer's coverage + entropy (12 B per position)
+    sum_only = rb + 8 * (L // 128) + 24 * (L // 8192) + 12 * (L % 8192)
     return {"pileup": rb + 4 * k * L + stats_out, "solo": rb + 4 * k * L + stats_out, "rc": rb + 4 * k * L,
             "rc_no_index": rb + 4 * k * L, "rc_indexed": rb + 4 * k * L,
             "pileup_no_index": rb + 4 * k * L + stats_out, "stats": 4 * k * L + stats_out, "solo_sum": sum_only}[kernel]
@@ -940,8 +941,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
                     if dom == "pileup" else
                     "k_pileup_solo (sparse sweep, kernel 1 and kernel 2 fused), one launch per contig per step"
                     if dom == "solo" else
-                    "k_pileup_solo summary-only sweep (kernels 1 + 2 fused, numpy's partials, no per-position "
-                    "output), one launch per contig per step"
+                    "the read-parallel summary-only kernels (k_sum_reads, k_sum_exact, k_sum_buffers, numpy's "
+                    "partials, no per-position output), per contig per step"
                     if dom == "solo_sum" else
                     "k_rc (kernel 1, into a zeroed scratch) + k_stats_lane (kernel 2, moves the counts out "
                     "and re-zeroes) per contig per step")
@@ -1004,8 +1005,8 @@ def run_config(cfg: str, ctx, group, args, rank: int, world: int, steps: int, wa
 
 
 def run_c5(ctx, group, args, rank: int, world: int, steps: int, warmup: int, launch: str) -> dict:
-    """C5 as --summarise runs it: the summary-only sweep (no per-position
-    output; main.py:469-499 prints six numbers per contig) is the step; the storing sweep (every
+    """C5 as --summarise runs it: the summary-only call (read-parallel, no
+    per-position output; main.py:469-499 prints six numbers per contig) is the step; the storing sweep (every
     count, coverage and entropy written, as the library API, rows and --summarise-with-bed need
     them) is timed after it on the same contigs and reported beside it as `storing`."""
     r = run_config("c5", ctx, group, args, rank, world, steps, warmup, launch, summarise=True, summary_only=True)

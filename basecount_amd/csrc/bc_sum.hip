@@ -166,7 +166,7 @@ __device__ __forceinline__ void tile_counts(const PileArgs& A, int64_t t, int la
 
 constexpr int kSumTr = 64;  // doubles of leaf transposition scratch per wave
 template <bool QUAL, int K>
-__global__ __launch_bounds__(256, 4) void k_sum_exact(PileArgs A) {
+__global__ __launch_bounds__(256, 2) void k_sum_exact(PileArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

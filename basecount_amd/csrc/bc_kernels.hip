@@ -605,15 +605,77 @@ __device__ __forceinline__ long long block_sum_i64(long long v, long long* s_red
     return r;
 }
 
+// The last, partial buffer of a reference (m < 8192 elements): numpy's generic pairwise tree
+// (pw_block) over the entropies staged in LDS (dynamic, m doubles), so the leaves are summed from
+// LDS instead of one dependent global load after another; every global load of the buffer is
+// issued at once.
+__device__ __forceinline__ void sum_tail_block(const int32_t* cov, const double* ent, int64_t L, double* part_ent,
+                                               long long* part_cov, long long* part_nz, int64_t chunk) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    double* s_ent = (double*)dyn;  // [m]
+    __shared__ long long s_red[8];
+    __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
+    __shared__ double s_val[2 << kLv];
+    const int64_t c0 = chunk * kNpBuf;
+    const int m = (int)(L - c0);  // 0 < m < 8192
+    const int t = threadIdx.x;
+    int cv[32];
+    double ev[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const int i = t + 256 * j;
+        cv[j] = i < m ? cov[c0 + i] : 0;
+        ev[j] = i < m ? ent[c0 + i] : 0.0;
+    }
+    long long cs = 0, nz = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        cs += cv[j];
+        nz += cv[j] != 0;
+        const int i = t + 256 * j;
+        if (i < m) s_ent[i] = ev[j];
+    }
+    __syncthreads();
+    const double e = pw_block(s_ent, m, s_off, s_len, s_val);
+    for (int o = 32; o > 0; o >>= 1) {
+        cs += __shfl_down(cs, o);
+        nz += __shfl_down(nz, o);
+    }
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = cs;
+        s_red[4 + (t >> 6)] = nz;
+    }
+    __syncthreads();
+    if (t == 0) {
+        part_ent[chunk] = e;
+        part_cov[chunk] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        part_nz[chunk] = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sum_tail(const int32_t* cov, const double* ent, int64_t L,
+                                                  double* part_ent, long long* part_cov, long long* part_nz,
+                                                  int64_t chunk, int32_t* hdr, int32_t hval) {
+    if (threadIdx.x == 0 && hdr) *hdr = hval;
+    sum_tail_block(cov, ent, L, part_ent, part_cov, part_nz, chunk);
+}
+
 // one workgroup (256 threads) per 8192 buffer: entropy pairwise sum, exact coverage sum, nnz.
 // A full buffer issues all its loads up front (8 x 16 B of coverage and 16 x 16 B of entropy per
 // thread) before any reduction, so a workgroup has its whole 96 KiB in flight at once; the
 // coverage sum and the non-zero count share one block reduction.
-// (hdr: block 0 also writes the work header, the fold's count of quarter buffers: no memset launch)
+// (hdr: block 0 also writes the work header, the fold's count of quarter buffers: no memset launch;
+// STAGE_TAIL: the last block is the reference's partial buffer, summed as k_sum_tail does, in
+// the same launch — the dynamic LDS then holds its entropies)
+template <bool STAGE_TAIL>
 __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const double* ent, int64_t L,
                                                     double* part_ent, long long* part_cov, long long* part_nz,
                                                     int64_t first_chunk, int32_t* hdr, int32_t hval) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && hdr) *hdr = hval;
+    if (STAGE_TAIL && blockIdx.x == gridDim.x - 1) {  // (uniform)
+        sum_tail_block(cov, ent, L, part_ent, part_cov, part_nz, first_chunk + blockIdx.x);
+        return;
+    }
     __shared__ double s_wave[4];
     __shared__ long long s_red[8];
     __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
@@ -644,55 +706,6 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const int32_t* cov, const do
         e = (m == kNpBuf) ? pw_full8192([&](int i) { return ent[c0 + i]; }, s_wave)
                           : pw_block(ent + c0, m, s_off, s_len, s_val);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        cs += __shfl_down(cs, o);
-        nz += __shfl_down(nz, o);
-    }
-    if ((t & 63) == 0) {
-        s_red[t >> 6] = cs;
-        s_red[4 + (t >> 6)] = nz;
-    }
-    __syncthreads();
-    if (t == 0) {
-        part_ent[chunk] = e;
-        part_cov[chunk] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-        part_nz[chunk] = (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
-    }
-}
-
-// The last, partial buffer of a reference (m < 8192 elements): numpy's generic pairwise tree
-// (pw_block) over the entropies staged in LDS, so the leaves are summed from LDS instead of one
-// dependent global load after another; every global load of the buffer is issued at once.
-__global__ __launch_bounds__(256) void k_sum_tail(const int32_t* cov, const double* ent, int64_t L,
-                                                  double* part_ent, long long* part_cov, long long* part_nz,
-                                                  int64_t chunk, int32_t* hdr, int32_t hval) {
-    if (threadIdx.x == 0 && hdr) *hdr = hval;
-    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-    double* s_ent = (double*)dyn;  // [m]
-    __shared__ long long s_red[8];
-    __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
-    __shared__ double s_val[2 << kLv];
-    const int64_t c0 = chunk * kNpBuf;
-    const int m = (int)(L - c0);  // 0 < m < 8192
-    const int t = threadIdx.x;
-    int cv[32];
-    double ev[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        const int i = t + 256 * j;
-        cv[j] = i < m ? cov[c0 + i] : 0;
-        ev[j] = i < m ? ent[c0 + i] : 0.0;
-    }
-    long long cs = 0, nz = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        cs += cv[j];
-        nz += cv[j] != 0;
-        const int i = t + 256 * j;
-        if (i < m) s_ent[i] = ev[j];
-    }
-    __syncthreads();
-    const double e = pw_block(s_ent, m, s_off, s_len, s_val);
     for (int o = 32; o > 0; o >>= 1) {
         cs += __shfl_down(cs, o);
         nz += __shfl_down(nz, o);
@@ -1052,20 +1065,32 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
     }
     const int64_t n = hi - lo + 1;
     const int64_t k1 = (n - 1) / 2, k2 = n / 2;
-    __shared__ unsigned long long s_med[3][2];  // the k1-th / k2-th smallest of cov, ent, sec
-    if (n <= 64 * kAmpSortE) {
-        // windows of amplicon size (C4: ~300 positions): waves 0-2 each sort one array's keys in
-        // registers (the doubles are >= 0, so their bit patterns order like their values)
+    __shared__ unsigned long long s_med[3][2];
+    constexpr int kWin = 64 * kAmpSortE;
+    // windows of amplicon size (C4: ~300 positions): the three arrays staged in LDS once (every
+    // load issued at once), then the sorts, the sums and numpy's pairwise means read LDS only
+    __shared__ int32_t s_c[kWin];
+    __shared__ double s_e[kWin], s_s[kWin];
+    const bool sorted = n <= kWin;  // (uniform)
+    if (sorted) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            s_c[i] = cov[lo + i];
+            s_e[i] = ent[lo + i];
+            s_s[i] = sec[lo + i];
+        }
+        __syncthreads();
+        // waves 0-2 each sort one array's keys in registers (the doubles are >= 0, so their bit
+        // patterns order like their values)
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         if (wave < 3) {
             unsigned long long v[kAmpSortE];
 #pragma unroll
-            for (int r = 0; r < kAmpSortE; ++r) {  // (coalesced: the input order does not matter)
-                const int64_t i = (int64_t)r * 64 + lane;
+            for (int r = 0; r < kAmpSortE; ++r) {  // (the input order does not matter)
+                const int i = r * 64 + lane;
                 v[r] = ~0ull;
                 if (i < n)
-                    v[r] = wave == 0 ? (unsigned long long)(uint32_t)cov[lo + i]
-                                     : (unsigned long long)__double_as_longlong((wave == 1 ? ent : sec)[lo + i]);
+                    v[r] = wave == 0 ? (unsigned long long)(uint32_t)s_c[i]
+                                     : (unsigned long long)__double_as_longlong((wave == 1 ? s_e : s_s)[i]);
             }
             wave_bitonic<kAmpSortE>(v);
             const unsigned long long a = wave_kth<kAmpSortE>(v, k1), b = wave_kth<kAmpSortE>(v, k2);
@@ -1078,14 +1103,13 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
     }
     // coverage: exact integer mean, median via 32-bit select
     long long cs = 0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) cs += cov[lo + i];
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) cs += sorted ? s_c[i] : cov[lo + i];
     cs = block_sum_i64(cs, s_red);
-    const bool sorted = n <= 64 * kAmpSortE;  // (uniform)
     auto ckey = [&](int64_t i) { return (unsigned long long)(uint32_t)cov[lo + i]; };
     const double c_a = sorted ? (double)s_med[0][0] : (double)radix_select(ckey, n, k1, 32, s_hist, s_sel);
     const double c_b = sorted ? (double)s_med[0][1]
                               : (k2 != k1) ? (double)radix_select(ckey, n, k2, 32, s_hist, s_sel) : c_a;
-    const double* vals[2] = {ent + lo, sec + lo};
+    const double* vals[2] = {sorted ? s_e : ent + lo, sorted ? s_s : sec + lo};
     double means[2], meds[2];
     for (int q = 0; q < 2; ++q) {
         const double* a = vals[q];
@@ -1238,9 +1262,15 @@ hipError_t launch_summary_partials(hipStream_t s, const int32_t* cov, const doub
     const int64_t nfull = L / kNpBuf;  // whole buffers: k_sum_chunks; the partial one: k_sum_tail
     const bool chunks = nfull > first_chunk, tail = nc > nfull && nfull >= first_chunk;
     if (!chunks && !tail) return hipMemsetD32Async((hipDeviceptr_t)P.hdr, hval, 1, s);
+    const size_t tail_lds = (size_t)(L - nfull * kNpBuf) * sizeof(double);
+    if (chunks && tail && nfull - first_chunk <= 64) {  // a short reference: whole buffers and tail in one launch
+        hipLaunchKernelGGL(k_sum_chunks<true>, dim3((unsigned)(nfull - first_chunk + 1)), dim3(256), tail_lds, s, cov,
+                           ent, L, P.ent, P.cov, P.nz, first_chunk, P.hdr, hval);
+        return hipGetLastError();
+    }
     if (chunks)
-        hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)(nfull - first_chunk)), dim3(256), 0, s, cov, ent, L, P.ent,
-                           P.cov, P.nz, first_chunk, P.hdr, hval);
+        hipLaunchKernelGGL(k_sum_chunks<false>, dim3((unsigned)(nfull - first_chunk)), dim3(256), 0, s, cov, ent, L,
+                           P.ent, P.cov, P.nz, first_chunk, P.hdr, hval);
     if (tail)
         hipLaunchKernelGGL(k_sum_tail, dim3(1), dim3(256), (size_t)(L - nfull * kNpBuf) * sizeof(double), s, cov, ent,
                            L, P.ent, P.cov, P.nz, nfull, chunks ? nullptr : P.hdr, hval);

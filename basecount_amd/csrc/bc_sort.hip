@@ -4,7 +4,11 @@
 // (count.cpp:22-97 adds one per event), but the fast kernels do: the tiled k_pileup walks a
 // contiguous range of reads per tile and the read-chunked k_rc stages a chunk's contiguous
 // sequence.  An unsorted batch (reads of one reference in any order) is therefore put in start
-// order here, with no host round trip:
+// order here, with no host round trip.  The default is the bucketed sort (k_bkt_*, below): no
+// global atomics, per-block LDS histograms of the starts' high bits, one block per bucket sorting
+// by the low bits, the sequence copied in destination order (C3 in random order: 163 -> 100 us).
+// The counting sort with one global atomic per read (below) remains for references too long for
+// the buckets (more than 2^24 starts) and, with `exact`, for reads of very different lengths:
 //   1. k_sort_count    counting sort by start position: one atomic per read on its position's bin
 //                      (the returned old value is the read's rank inside the bin), the read's
 //                      query length from its CIGAR (M/I/=/X), its fields packed in 32 bytes;
@@ -148,6 +152,16 @@ struct SortArgs {
     int64_t qual_bytes;
     int64_t nbins;      // bins: starts in [0, nbins - 1)
     uint32_t* qmax;     // the batch's largest query length (device word; fast variant)
+    // the bucketed variant (k_bkt_*): buckets of 2^wbits starts, nbkt of them; block b of the
+    // count and scatter passes takes reads [b * chunk, (b + 1) * chunk)
+    uint32_t* mat;      // [nblk][nbkt]: reads of bucket h in block b
+    uint32_t* bbase;    // [nbkt + 1]: the first sorted slot of bucket h
+    uint32_t* qlen;     // [n] query length of read i
+    uint32_t* bstat;    // [nblk][2]: block b's largest query length, its flags
+    uint4* brec;        // [n] {pos, cig_beg, seq_nib, cig_n | qlen << 16} in bucket order
+    uint4* srec;        // [n] the same in start order
+    int64_t chunk;
+    int nblk, nbkt, wbits;
 };
 
 
@@ -364,15 +378,393 @@ __global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
     if (sub == 0) A.o_seq_nib[j] = 2 * off + (sn & 1u);
 }
 
+// ---- the bucketed sort (no global atomics): starts binned by their high bits with per-block
+// LDS histograms, each bucket then sorted by its low bits in one block, the sequence copied in
+// start order.
+//   k_bkt_count    block b: its reads' bucket histogram in LDS -> row b of mat (every entry
+//                  written), each read's query length, the block's largest one and its range flag;
+//   k_bkt_scatter  block b: every bucket's total and the count of blocks before b from the rows
+//                  (coalesced, L2-resident), their scan in LDS, then each read's slot in (bucket,
+//                  block) from an LDS atomic with return; its 16-byte record written there.  Block
+//                  0 also writes every bucket's first slot and folds the block stats into the
+//                  batch's largest query length and the overflow word;
+//   k_bkt_rank     one block per bucket, the bucket's records in registers: LDS counting sort by
+//                  the low bits (histogram, scan, ranks), the records written in start order;
+//   k_bkt_copy     4 lanes per sorted slot: fields, sequence and qualities into fixed slots, so
+//                  a wave writes whole lines of the copy (destination order).
+// Measured and dropped: rank and copy fused (one block per bucket staging its records in LDS and
+// copying them): 79 us against 10 + 53; the matrix scanned by scan_u32 (3 launches, 14 us)
+// instead of each scatter block summing the rows itself.
+constexpr int kBktThreads = 1024;  // count / scatter blocks
+constexpr int kBktGroup = 8;       // scatter: buckets per lane and rows per wave whose count loads
+constexpr int kBktRows = 4;        // are in flight together
+constexpr int kRankThreads = 512;
+constexpr int kRankRegs = 8;       // records per rank thread held in registers
+constexpr int kBktMax = 4096;      // buckets (LDS words of the count / scatter passes)
+constexpr int kBktLowMax = 4096;   // low-bit bins of one bucket (2^12)
+constexpr uint32_t kQlenMax = 0xFFFFu;  // query lengths packed in 16 bits
+
+__device__ __forceinline__ uint32_t bkt_pos(const SortArgs& A, int64_t i, bool& bad) {
+    int32_t p = A.pos[i];
+    bad = p < 0 || (int64_t)p >= A.nbins - 1;
+    return bad ? 0u : (uint32_t)p;
+}
+
+// exclusive scan of s[0, m) in LDS by an NT-thread block (m <= NT * E); ws: NT / 64 words
+template <int NT, int E>
+__device__ __forceinline__ void lds_scan_excl(uint32_t* s, int m, uint32_t* ws) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t v[E], tot = 0;
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        const int at = t * E + k;
+        v[k] = at < m ? s[at] : 0u;
+        tot += v[k];
+    }
+    uint32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - tot;
+    for (int w = 0; w < wave; ++w) run += ws[w];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        const int at = t * E + k;
+        if (at < m) s[at] = run;
+        run += v[k];
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBktThreads) void k_bkt_count(SortArgs A) {
+    __shared__ uint32_t hist[kBktMax];
+    __shared__ uint32_t wmax[kBktThreads / 64], wflag[kBktThreads / 64];
+    const int H = A.nbkt;
+    const int64_t beg = (int64_t)blockIdx.x * A.chunk;
+    const int64_t end = beg + A.chunk < A.n ? beg + A.chunk : A.n;
+    for (int h = threadIdx.x; h < H; h += kBktThreads) hist[h] = 0u;
+    __syncthreads();
+    uint32_t qm = 0, fl = 0;
+    constexpr int B = 8;  // reads per thread whose loads are in flight together
+    for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)B * kBktThreads) {
+        uint32_t p[B], cb[B], cn[B];
+        bool bad[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int64_t i = i0 + (int64_t)u * kBktThreads;
+            p[u] = 0u, cb[u] = 0u, cn[u] = 0u, bad[u] = false;
+            if (i < end) {
+                p[u] = bkt_pos(A, i, bad[u]);
+                cb[u] = A.cig_beg[i];
+                cn[u] = A.cig_n[i];
+            }
+        }
+        uint32_t w[B][8];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[u][k] = (uint32_t)k < cn[u] ? A.cigar[cb[u] + k] : 0u;
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int64_t i = i0 + (int64_t)u * kBktThreads;
+            if (i >= end) break;
+            uint32_t q = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (qcons(w[u][k] & 15u)) q += w[u][k] >> 4;
+            for (uint32_t k = 8; k < cn[u]; ++k) {
+                const uint32_t x = A.cigar[cb[u] + k];
+                if (qcons(x & 15u)) q += x >> 4;
+            }
+            A.qlen[i] = q;
+            qm = q > qm ? q : qm;
+            fl |= (bad[u] ? 2u : 0u) | (cn[u] > 0xFFFFu ? 4u : 0u);  // (cig_n is packed in 16 bits)
+            atomicAdd(&hist[p[u] >> A.wbits], 1u);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(qm, o), f = __shfl_xor(fl, o);
+        qm = y > qm ? y : qm;
+        fl |= f;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = qm, wflag[threadIdx.x >> 6] = fl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kBktThreads / 64; ++k) {
+            qm = wmax[k] > qm ? wmax[k] : qm;
+            fl |= wflag[k];
+        }
+        A.bstat[2 * blockIdx.x] = qm;
+        A.bstat[2 * blockIdx.x + 1] = fl;
+    }
+    for (int h = threadIdx.x; h < H; h += kBktThreads) A.mat[(int64_t)blockIdx.x * H + h] = hist[h];
+}
+
+// slot bytes of the fixed-slot copy (relay_slot) and whether they fit: the flags of the batch
+__device__ __forceinline__ uint32_t bkt_flags(const SortArgs& A, uint32_t qm, uint32_t fl) {
+    if (qm >= kQlenMax || (uint64_t)relay_slot(qm) * (uint64_t)A.n > (uint64_t)A.cap) fl |= 4u;
+    return fl;
+}
+
+__global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
+    __shared__ uint32_t next[kBktMax], pre[kBktMax];
+    __shared__ uint32_t ws[kBktThreads / 64];
+    __shared__ uint32_t rq, rf;
+    const int H = A.nbkt, nb = A.nblk, b = blockIdx.x;
+    if (threadIdx.x == 0) rq = 0u, rf = 0u;
+    const int64_t beg = (int64_t)b * A.chunk;
+    const int64_t end = beg + A.chunk < A.n ? beg + A.chunk : A.n;
+    // bucket h's total and its reads in blocks before b, from the count rows: wave v takes rows
+    // v, v + 16, ..., lane the buckets lane + 64 m (every load of a lane issued before its adds),
+    // the 16 waves' partial sums meet in LDS
+    for (int h = threadIdx.x; h < H; h += kBktThreads) next[h] = 0u, pre[h] = 0u;
+    __syncthreads();
+    {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        constexpr int NW = kBktThreads / 64;
+        for (int h0 = 0; h0 < H; h0 += 64 * kBktGroup) {
+            uint32_t tot[kBktGroup], before[kBktGroup];
+#pragma unroll
+            for (int m = 0; m < kBktGroup; ++m) tot[m] = 0u, before[m] = 0u;
+            for (int r0 = wave; r0 < nb; r0 += NW * kBktRows) {
+                uint32_t v[kBktRows][kBktGroup];
+#pragma unroll
+                for (int u = 0; u < kBktRows; ++u)
+#pragma unroll
+                    for (int m = 0; m < kBktGroup; ++m) {
+                        const int r = r0 + u * NW, h = h0 + 64 * m + lane;
+                        v[u][m] = r < nb && h < H ? A.mat[(int64_t)r * H + h] : 0u;
+                    }
+#pragma unroll
+                for (int u = 0; u < kBktRows; ++u)
+#pragma unroll
+                    for (int m = 0; m < kBktGroup; ++m) {
+                        tot[m] += v[u][m];
+                        before[m] += r0 + u * NW < b ? v[u][m] : 0u;
+                    }
+            }
+#pragma unroll
+            for (int m = 0; m < kBktGroup; ++m) {
+                const int h = h0 + 64 * m + lane;
+                if (h < H && tot[m]) atomicAdd(&next[h], tot[m]);
+                if (h < H && before[m]) atomicAdd(&pre[h], before[m]);
+            }
+        }
+    }
+    __syncthreads();
+    lds_scan_excl<kBktThreads, kBktMax / kBktThreads>(next, H, ws);
+    if (b == 0) {  // every bucket's first slot; the batch's largest query length and flags
+        for (int h = threadIdx.x; h < H; h += kBktThreads) A.bbase[h] = next[h];
+        uint32_t qm = 0, fl = 0;
+        for (int k = threadIdx.x; k < nb; k += kBktThreads) {
+            qm = A.bstat[2 * k] > qm ? A.bstat[2 * k] : qm;
+            fl |= A.bstat[2 * k + 1];
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t y = __shfl_xor(qm, o), f = __shfl_xor(fl, o);
+            qm = y > qm ? y : qm;
+            fl |= f;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMax(&rq, qm);
+            atomicOr(&rf, fl);
+        }
+        __syncthreads();  // (uniform: b == 0 for the whole block)
+        if (threadIdx.x == 0) {
+            A.bbase[H] = (uint32_t)A.n;
+            *A.qmax = rq;
+            *A.overflow = bkt_flags(A, rq, rf);
+        }
+        const size_t pad0 = A.cap, pad1 = ((size_t)A.cap + 15) / 16 * 16 + 16;  // seq_event_bytes(cap): zero
+        for (size_t at = pad0 + threadIdx.x; at < pad1; at += kBktThreads) A.o_seq[at] = 0;
+    }
+    for (int h = threadIdx.x; h < H; h += kBktThreads) next[h] += pre[h];
+    __syncthreads();
+    constexpr int B = 8;
+    for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)B * kBktThreads) {
+        uint4 rec[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int64_t i = i0 + (int64_t)u * kBktThreads;
+            rec[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (i < end) {
+                bool bad;
+                const uint32_t q = A.qlen[i];
+                rec[u] = make_uint4(bkt_pos(A, i, bad), A.cig_beg[i], A.seq_nib[i],
+                                    (A.cig_n[i] & 0xFFFFu) | ((q < kQlenMax ? q : kQlenMax) << 16));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int64_t i = i0 + (int64_t)u * kBktThreads;
+            if (i >= end) break;
+            const uint32_t j = atomicAdd(&next[rec[u].x >> A.wbits], 1u);
+            A.brec[j] = rec[u];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
+    __shared__ uint32_t cnt[kBktLowMax];
+    __shared__ uint32_t ws[kRankThreads / 64];
+    const int h = blockIdx.x, t = threadIdx.x;
+    const uint32_t bs = A.bbase[h], be = A.bbase[h + 1];
+    const int W = 1 << A.wbits;
+    const uint32_t lo_mask = (uint32_t)W - 1u;
+    uint4 rec[kRankRegs];  // the bucket's first kRankRegs * kRankThreads records
+#pragma unroll
+    for (int k = 0; k < kRankRegs; ++k) {
+        const uint32_t r = bs + t + k * kRankThreads;
+        rec[k] = r < be ? A.brec[r] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    for (int k = t; k < W; k += kRankThreads) cnt[k] = 0u;
+    __syncthreads();
+    const uint32_t more = bs + kRankRegs * kRankThreads;  // records past the registers (large buckets)
+#pragma unroll
+    for (int k = 0; k < kRankRegs; ++k)
+        if (bs + t + k * kRankThreads < be) atomicAdd(&cnt[rec[k].x & lo_mask], 1u);
+    for (uint32_t r = more + t; r < be; r += kRankThreads) atomicAdd(&cnt[A.brec[r].x & lo_mask], 1u);
+    __syncthreads();
+    lds_scan_excl<kRankThreads, kBktLowMax / kRankThreads>(cnt, W, ws);
+#pragma unroll
+    for (int k = 0; k < kRankRegs; ++k)
+        if (bs + t + k * kRankThreads < be) A.srec[bs + atomicAdd(&cnt[rec[k].x & lo_mask], 1u)] = rec[k];
+    for (uint32_t r = more + t; r < be; r += kRankThreads) {
+        const uint4 x = A.brec[r];
+        A.srec[bs + atomicAdd(&cnt[x.x & lo_mask], 1u)] = x;
+    }
+}
+
+// R sorted reads per 4-lane group (lane `sub` of the group): read r = record a[r] for slot jj[r]
+// (ok[r]: uniform in the group).  Fields (lane r & 3 writes read r's), the aligned sequence into
+// fixed slots (two source words and a funnel shift per output word; every source word of the
+// unrolled part requested first) and the qualities; the new nibble index keeps the old parity.
+template <int R>
+__device__ __forceinline__ void copy_reads(const SortArgs& A, const uint4 (&a)[R], const uint32_t (&jj)[R],
+                                           const bool (&ok)[R], uint32_t sub, uint32_t slot) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (ok[r] && sub == ((uint32_t)r & 3u)) {
+            const uint32_t j = jj[r];
+            A.o_pos[j] = (int32_t)a[r].x;
+            A.o_cig_beg[j] = a[r].y;
+            A.o_cig_n[j] = a[r].w & 0xFFFFu;
+            A.o_seq_nib[j] = 2u * (slot * j) + (a[r].z & 1u);
+        }
+    uint32_t x[R][kRelayWords + 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t sn = a[r].z, words = ((((sn & 1u) + (a[r].w >> 16) + 1u) >> 1) + 3u) >> 2;
+        const uint32_t* s32 = (const uint32_t*)(A.seq + ((sn >> 1) & ~3u));
+#pragma unroll
+        for (int k = 0; k <= kRelayWords; ++k) {
+            const uint32_t w = sub + 4u * (uint32_t)k;
+            x[r][k] = (ok[r] && w <= words) ? s32[w] : 0u;  // (word `words`: the last shift's upper half)
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!ok[r]) continue;  // (uniform in the lane group)
+        const uint32_t j = jj[r];
+        const uint32_t sn = a[r].z, from = sn >> 1, words = ((((sn & 1u) + (a[r].w >> 16) + 1u) >> 1) + 3u) >> 2;
+        const uint32_t sh = (from & 3u) * 8u;
+        const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
+        uint32_t* d32 = (uint32_t*)(A.o_seq + slot * j);
+#pragma unroll
+        for (int k = 0; k < kRelayWords; ++k) {
+            const uint32_t w = sub + 4u * (uint32_t)k;
+            const uint32_t nxt = __shfl_down(x[r][k], 1, 4), wrap = __shfl(x[r][k + 1], 0, 4);
+            if (w < words) d32[w] = __builtin_amdgcn_alignbit(sub == 3u ? wrap : nxt, x[r][k], sh);
+        }
+        for (uint32_t w = sub + 4u * kRelayWords; w < words; w += 4)
+            d32[w] = __builtin_amdgcn_alignbit(s32[w + 1], s32[w], sh);
+        if (A.qual) {
+            const uint64_t qf = 2 * (uint64_t)from;
+            const uint32_t* q32 = (const uint32_t*)(A.qual + (qf & ~3ull));
+            const uint32_t qsh = (uint32_t)(qf & 3u) * 8u;
+            uint32_t* dq = (uint32_t*)(A.o_qual + 2 * (uint64_t)slot * (uint64_t)j);
+            const uint64_t q0 = qf & ~3ull;
+            for (uint32_t w = sub; w < 2 * words; w += 4) {
+                if (q0 + 4ull * w + 8 <= (uint64_t)A.qual_bytes) {
+                    dq[w] = __builtin_amdgcn_alignbit(q32[w + 1], q32[w], qsh);
+                } else {  // the buffer's last bytes (the quality buffer has no padding)
+                    uint32_t v = 0;
+                    for (uint32_t bb = 0; bb < 4; ++bb) {
+                        const uint64_t at = qf + 4ull * w + bb;
+                        if (at < (uint64_t)A.qual_bytes) v |= (uint32_t)A.qual[at] << (8 * bb);
+                    }
+                    dq[w] = v;
+                }
+            }
+        }
+    }
+}
+
+// 4 lanes per sorted slot, kRelayReads slots per lane group, over every slot (after k_bkt_rank)
+__global__ __launch_bounds__(256) void k_bkt_copy(SortArgs A) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t sub = (uint32_t)g & 3u;
+    // a wave's 16 lane groups take 64 consecutive slots: group q of the wave, step r -> slot
+    // base + 16 r + q, so each store instruction writes 16 neighbouring slots
+    const int64_t wbase = (g >> 6) * 64, q = (g & 63) >> 2;
+    if (wbase >= A.n) return;
+    if (*A.overflow & 6u) return;  // bad starts / slots that do not fit: the caller runs the exact steps
+    const uint32_t slot = relay_slot(*A.qmax);
+    uint4 a[kRelayReads];
+    uint32_t jj[kRelayReads];
+    bool ok[kRelayReads];
+#pragma unroll
+    for (int r = 0; r < kRelayReads; ++r) {
+        const int64_t j = wbase + 16 * r + q;
+        ok[r] = j < A.n;
+        jj[r] = (uint32_t)j;
+        a[r] = ok[r] ? A.srec[j] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    copy_reads<kRelayReads>(A, a, jj, ok, sub, slot);
+}
+
+// The bucketed sort's shape: buckets of 2^wbits starts (at most 512 of them, or 4096 of 4096),
+// blocks of `chunk` reads, so that the count rows (blocks x buckets) stay within 65,536 words:
+// each scatter block reads them all.  ok = false: the counting sort with global atomics.
+struct BktPlan {
+    bool ok;
+    int wbits, nbkt, nblk;
+    int64_t chunk;
+};
+
+BktPlan bkt_plan(const bc_reads& r) {
+    BktPlan P{};
+    const int64_t n = r.n_reads, nbins = r.max_end + 2;
+    if (n <= 0 || n >= (int64_t)0xFFFFFFFFll || nbins <= 0) return P;
+    int w = 0;
+    while (w < 12 && (nbins + (1ll << w) - 1) >> w > 512) ++w;
+    const int64_t H = (nbins + (1ll << w) - 1) >> w;
+    if (H > kBktMax) return P;
+    P.wbits = w;
+    P.nbkt = (int)H;
+    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((n + 8191) / 8192, 65536 / H));
+    P.chunk = (n + nblk - 1) / nblk;
+    P.nblk = (int)((n + P.chunk - 1) / P.chunk);
+    P.ok = true;
+    return P;
+}
+
 struct SortLayout {
-    size_t bins, rec, src, perm, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, total;
+    size_t bins, rec, src, perm, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, mat, bstat, bbase, total;
     int64_t nbins;
     uint32_t cap;
+    BktPlan bkt;
 };
 
 SortLayout sort_layout(const bc_reads& r) {
     SortLayout L{};
     const int64_t n = r.n_reads;
+    L.bkt = bkt_plan(r);
+    const int64_t mat_words = L.bkt.ok ? (int64_t)L.bkt.nbkt * L.bkt.nblk : 0;
     L.nbins = r.max_end + 2;  // every start <= max_end
     // every read takes its aligned bases' bytes rounded up to 4 (+ 1 for an odd start)
     L.cap = (uint32_t)std::min<int64_t>(r.seq_bytes + 5 * n + 16, 0xFFFFFFF0ll);
@@ -395,6 +787,9 @@ SortLayout sort_layout(const bc_reads& r) {
     L.words = take(16);  // total, overflow
     L.o_seq = take(seq_event_bytes(L.cap));
     L.o_qual = r.qual ? take(2 * (size_t)L.cap + 32) : 0;
+    L.mat = take(4 * (size_t)mat_words);
+    L.bstat = take(8 * (size_t)(L.bkt.ok ? L.bkt.nblk : 0));
+    L.bbase = take(4 * (size_t)(L.bkt.ok ? L.bkt.nbkt + 1 : 0));
     L.total = off;
     return L;
 }
@@ -437,22 +832,45 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     A.qmax = A.total + 2;
     uint32_t* tmp = (uint32_t*)(b + L.tmp);
     const unsigned blocks = (unsigned)((r.n_reads + 255) / 256);
-    hipError_t e = hipMemsetAsync(A.bins, 0, 4 * (size_t)L.nbins, s);
-    if (e == hipSuccess) e = hipMemsetAsync(A.total, 0, 16, s);  // total, overflow, qmax
-    // the sorted sequence's padding past cap (BC_SEQ_EVENT) is zero
-    if (e == hipSuccess) e = hipMemsetAsync(A.o_seq + L.cap, 0, seq_event_bytes(L.cap) - L.cap, s);
-    if (e != hipSuccess) return e;
-    if (exact) hipLaunchKernelGGL(k_sort_count<false>, dim3(blocks), dim3(256), 0, s, A);
-    else hipLaunchKernelGGL(k_sort_count<true>, dim3(blocks), dim3(256), 0, s, A);
-    if ((e = scan_u32(s, A.bins, L.nbins, tmp, nullptr)) != hipSuccess) return e;
-    if (exact) hipLaunchKernelGGL(k_sort_perm, dim3(blocks), dim3(256), 0, s, A);
-    if (!exact) {
-        const int64_t groups = (r.n_reads + kRelayReads - 1) / kRelayReads;
-        hipLaunchKernelGGL(k_sort_relay, dim3((unsigned)((groups * 4 + 255) / 256)), dim3(256), 0, s, A);
+    static const bool bkt_off = [] {  // diagnostic A/B: BC_SORT_BKT=0 runs the global-atomic count
+        const char* v = std::getenv("BC_SORT_BKT");
+        return v && v[0] == '0';
+    }();
+    hipError_t e = hipSuccess;
+    if (!exact && L.bkt.ok && !bkt_off) {
+        A.mat = (uint32_t*)(b + L.mat);
+        A.qlen = A.src;
+        A.bstat = (uint32_t*)(b + L.bstat);
+        A.bbase = (uint32_t*)(b + L.bbase);
+        A.brec = A.rec;
+        A.srec = A.rec + r.n_reads;
+        A.chunk = L.bkt.chunk;
+        A.nblk = L.bkt.nblk;
+        A.nbkt = L.bkt.nbkt;
+        A.wbits = L.bkt.wbits;
+        hipLaunchKernelGGL(k_bkt_count, dim3((unsigned)A.nblk), dim3(kBktThreads), 0, s, A);
+        hipLaunchKernelGGL(k_bkt_scatter, dim3((unsigned)A.nblk), dim3(kBktThreads), 0, s, A);
+        hipLaunchKernelGGL(k_bkt_rank, dim3((unsigned)A.nbkt), dim3(kRankThreads), 0, s, A);
+        const int64_t waves = (r.n_reads + 63) / 64;
+        hipLaunchKernelGGL(k_bkt_copy, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, A);
     } else {
-        hipLaunchKernelGGL(k_sort_gather, dim3(blocks), dim3(256), 0, s, A);
-        if ((e = scan_u32(s, A.o_bytes, r.n_reads, tmp, A.total)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sort_seq, dim3((unsigned)((r.n_reads * 16 + 255) / 256)), dim3(256), 0, s, A);
+        e = hipMemsetAsync(A.bins, 0, 4 * (size_t)L.nbins, s);
+        if (e == hipSuccess) e = hipMemsetAsync(A.total, 0, 16, s);  // total, overflow, qmax
+        // the sorted sequence's padding past cap (BC_SEQ_EVENT) is zero
+        if (e == hipSuccess) e = hipMemsetAsync(A.o_seq + L.cap, 0, seq_event_bytes(L.cap) - L.cap, s);
+        if (e != hipSuccess) return e;
+        if (exact) hipLaunchKernelGGL(k_sort_count<false>, dim3(blocks), dim3(256), 0, s, A);
+        else hipLaunchKernelGGL(k_sort_count<true>, dim3(blocks), dim3(256), 0, s, A);
+        if ((e = scan_u32(s, A.bins, L.nbins, tmp, nullptr)) != hipSuccess) return e;
+        if (exact) hipLaunchKernelGGL(k_sort_perm, dim3(blocks), dim3(256), 0, s, A);
+        if (!exact) {
+            const int64_t groups = (r.n_reads + kRelayReads - 1) / kRelayReads;
+            hipLaunchKernelGGL(k_sort_relay, dim3((unsigned)((groups * 4 + 255) / 256)), dim3(256), 0, s, A);
+        } else {
+            hipLaunchKernelGGL(k_sort_gather, dim3(blocks), dim3(256), 0, s, A);
+            if ((e = scan_u32(s, A.o_bytes, r.n_reads, tmp, A.total)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_sort_seq, dim3((unsigned)((r.n_reads * 16 + 255) / 256)), dim3(256), 0, s, A);
+        }
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     out = r;

@@ -1107,8 +1107,8 @@ def run_split(ctx, group, steps: int, warmup: int) -> dict:
 
 def run_unsorted(ctx, args, reps: int = 20) -> dict:
     """C3's reads in random order (an unsorted BAM's batch, main.py:127 consumes file order):
-    the event-parallel k_count (+ k_stats) path against the device sort (bc_reads_sort: radix
-    sort of the starts + the sequence relayed into fixed slots) followed by the sorted path
+    the event-parallel k_count (+ k_stats) path against the device sort (bc_reads_sort: bucketed
+    sort of the starts + the sequence copied into fixed slots) followed by the sorted path
     (k_rc + k_stats, single pass, as the CLI runs it).  Each step starts from the raw unsorted batch in HBM; parity of both against the
     oracle; the same step on the coordinate-sorted C3 batch is measured beside it."""
     import oracle as O
@@ -1181,8 +1181,9 @@ def run_unsorted(ctx, args, reps: int = 20) -> dict:
             "event_parallel_step_us": ep_us,
             "event_parallel": "k_count (event-parallel kernel 1, global atomics) + k_stats, from the unsorted batch",
             "sort_us": sort_us, "sorted_step_us": ss_us, "sort_then_sorted_path_us": sort_us + ss_us,
-            "sorted_path": "bc_reads_sort (device: radix sort of the starts, then the reads' fields and "
-                           "sequence relayed into fixed slots in start order) then k_rc + k_stats (single pass)",
+            "sorted_path": "bc_reads_sort (device bucketed sort: per-block LDS histograms of the starts' high "
+                           "bits, one block per bucket sorting by the low bits, then the reads' fields and "
+                           "sequence copied into fixed slots in start order) then k_rc + k_stats (single pass)",
             "sorted_input_step_us": si_us,
             "ratio_to_sorted_input": (sort_us + ss_us) / si_us,
             "parity_vs_oracle": ok_ep and ok_s}

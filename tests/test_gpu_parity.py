@@ -342,8 +342,8 @@ def test_reads_index_on_device_slices(ctx, shape):
                                                (75, 6_000, 40_000, 20, True), (76, 3_000, 60_000, 0, False),
                                                (77, 500, 3, 0, False)])
 def test_device_sort_of_unsorted_batch(ctx, seed, L, n, mbq, qual):
-    """bc_reads_sort: an unsorted batch put in start order on the device (radix sort of the
-    starts + the sequence / quality relay into fixed slots); the sorted copy's starts are
+    """bc_reads_sort: an unsorted batch put in start order on the device (bucketed sort of the
+    starts + the sequence / quality copy into fixed slots); the sorted copy's starts are
     non-decreasing, it keeps every read, and every kernel shape on it gives the unsorted batch's
     counts (count.cpp's sums do not depend on the order)."""
     rng = np.random.default_rng(seed)
@@ -374,6 +374,39 @@ def test_device_sort_of_unsorted_batch(ctx, seed, L, n, mbq, qual):
             assert ctx.range_error() == -1
             got = hist.download(np.int32, k * L).reshape(k, L)
             assert np.array_equal(got, exp[:, :k].T.astype(np.int32)), (shape, k)
+    r.free()
+
+
+@pytest.mark.parametrize("case", ["hot_start", "long_reference"])
+def test_device_sort_bucket_extremes(ctx, case):
+    """The bucketed sort's edges: 30,000 reads starting in 40 positions (one bucket holds far more
+    records than a rank block keeps in registers: the overflow loops), and a reference of 2^24 +
+    4,096 positions (too many starts for the buckets: the counting sort with global atomics).
+    Sorted starts, and the sorted copy counts as the unsorted batch does."""
+    rng = np.random.default_rng(93)
+    if case == "hot_start":
+        L, n = 5_000, 30_000
+        b = random_batch(rng, L, n, sort=False, starts=lambda g, span: int(g.integers(200, 240)))
+    else:
+        L, n = (1 << 24) + 4_096, 2_000
+        b = random_batch(rng, L, n, sort=False, starts=lambda g, span: int(g.integers(L - 3_000, L - span)))
+    exp, (br, _) = O.bcount(L, 0, b)
+    assert br == -1
+    r = D.DeviceReads(ctx, b)
+    nb = ctx.sort_bytes(r)
+    mem = ctx.alloc(nb)
+    s = ctx.sort(r, mem.ptr, nb)
+    pos = np.zeros(s.n_reads, np.int32)
+    D.check(D.lib().bc_memcpy_d2h(ctx.h, pos.ctypes.data, s.pos, pos.nbytes))
+    ctx.sync()
+    assert np.array_equal(np.sort(b["pos"]), pos)
+    hist = ctx.alloc(4 * 5 * L)
+    hist.zero()
+    ctx.count(s, L, 0, 5, hist.ptr)
+    assert ctx.range_error() == -1
+    assert np.array_equal(hist.download(np.int32, 5 * L).reshape(5, L), exp[:, :5].T.astype(np.int32))
+    hist.free()
+    mem.free()
     r.free()
 
 

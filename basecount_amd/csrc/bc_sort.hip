@@ -6,7 +6,7 @@
 // sequence.  An unsorted batch (reads of one reference in any order) is therefore put in start
 // order here, with no host round trip.  The default is the bucketed sort (k_bkt_*, below): no
 // global atomics, per-block LDS histograms of the starts' high bits, one block per bucket sorting
-// by the low bits, the sequence copied in destination order (C3 in random order: 163 -> 100 us).
+// by the low bits, the sequence copied in destination order (C3 in random order: 164 -> 98 us).
 // The counting sort with one global atomic per read (below) remains for references too long for
 // the buckets (more than 2^24 starts) and, with `exact`, for reads of very different lengths:
 //   1. k_sort_count    counting sort by start position: one atomic per read on its position's bin
@@ -156,7 +156,6 @@ struct SortArgs {
     // count and scatter passes takes reads [b * chunk, (b + 1) * chunk)
     uint32_t* mat;      // [nblk][nbkt]: reads of bucket h in block b
     uint32_t* bbase;    // [nbkt + 1]: the first sorted slot of bucket h
-    uint32_t* qlen;     // [n] query length of read i
     uint32_t* bstat;    // [nblk][2]: block b's largest query length, its flags
     uint4* brec;        // [n] {pos, cig_beg, seq_nib, cig_n | qlen << 16} in bucket order
     uint4* srec;        // [n] the same in start order
@@ -381,15 +380,17 @@ __global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
 // ---- the bucketed sort (no global atomics): starts binned by their high bits with per-block
 // LDS histograms, each bucket then sorted by its low bits in one block, the sequence copied in
 // start order.
-//   k_bkt_count    block b: its reads' bucket histogram in LDS -> row b of mat (every entry
-//                  written), each read's query length, the block's largest one and its range flag;
+//   k_bkt_count    block b: its reads' bucket histogram in LDS (the starts alone) -> row b of mat
+//                  (every entry written);
 //   k_bkt_scatter  block b: every bucket's total and the count of blocks before b from the rows
 //                  (coalesced, L2-resident), their scan in LDS, then each read's slot in (bucket,
-//                  block) from an LDS atomic with return; its 16-byte record written there.  Block
-//                  0 also writes every bucket's first slot and folds the block stats into the
-//                  batch's largest query length and the overflow word;
+//                  block) from an LDS atomic with return; its 16-byte record (with the query
+//                  length from its CIGAR) written there; the block's largest query length and
+//                  flags; block 0 also writes every bucket's first slot;
 //   k_bkt_rank     one block per bucket, the bucket's records in registers: LDS counting sort by
 //                  the low bits (histogram, scan, ranks), the records written in start order;
+//                  block 0 folds the block stats into the batch's largest query length and the
+//                  overflow word;
 //   k_bkt_copy     4 lanes per sorted slot: fields, sequence and qualities into fixed slots, so
 //                  a wave writes whole lines of the copy (destination order).
 // Measured and dropped: rank and copy fused (one block per bucket staging its records in LDS and
@@ -442,65 +443,37 @@ __device__ __forceinline__ void lds_scan_excl(uint32_t* s, int m, uint32_t* ws) 
 
 __global__ __launch_bounds__(kBktThreads) void k_bkt_count(SortArgs A) {
     __shared__ uint32_t hist[kBktMax];
-    __shared__ uint32_t wmax[kBktThreads / 64], wflag[kBktThreads / 64];
     const int H = A.nbkt;
     const int64_t beg = (int64_t)blockIdx.x * A.chunk;
     const int64_t end = beg + A.chunk < A.n ? beg + A.chunk : A.n;
+    constexpr int B = 8;  // reads per thread whose loads are in flight together
+    uint32_t p[B];
+    bool in[B];
+    int64_t i0 = beg + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < B; ++u) {  // the first round's starts requested before the histogram is cleared
+        const int64_t i = i0 + (int64_t)u * kBktThreads;
+        bool bad;
+        in[u] = i < end;
+        p[u] = in[u] ? bkt_pos(A, i, bad) : 0u;
+    }
     for (int h = threadIdx.x; h < H; h += kBktThreads) hist[h] = 0u;
     __syncthreads();
-    uint32_t qm = 0, fl = 0;
-    constexpr int B = 8;  // reads per thread whose loads are in flight together
-    for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)B * kBktThreads) {
-        uint32_t p[B], cb[B], cn[B];
-        bool bad[B];
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            const int64_t i = i0 + (int64_t)u * kBktThreads;
-            p[u] = 0u, cb[u] = 0u, cn[u] = 0u, bad[u] = false;
-            if (i < end) {
-                p[u] = bkt_pos(A, i, bad[u]);
-                cb[u] = A.cig_beg[i];
-                cn[u] = A.cig_n[i];
-            }
-        }
-        uint32_t w[B][8];
+    for (;;) {
 #pragma unroll
         for (int u = 0; u < B; ++u)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) w[u][k] = (uint32_t)k < cn[u] ? A.cigar[cb[u] + k] : 0u;
+            if (in[u]) atomicAdd(&hist[p[u] >> A.wbits], 1u);
+        i0 += (int64_t)B * kBktThreads;
+        if (i0 - threadIdx.x >= end) break;  // (uniform)
 #pragma unroll
         for (int u = 0; u < B; ++u) {
             const int64_t i = i0 + (int64_t)u * kBktThreads;
-            if (i >= end) break;
-            uint32_t q = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (qcons(w[u][k] & 15u)) q += w[u][k] >> 4;
-            for (uint32_t k = 8; k < cn[u]; ++k) {
-                const uint32_t x = A.cigar[cb[u] + k];
-                if (qcons(x & 15u)) q += x >> 4;
-            }
-            A.qlen[i] = q;
-            qm = q > qm ? q : qm;
-            fl |= (bad[u] ? 2u : 0u) | (cn[u] > 0xFFFFu ? 4u : 0u);  // (cig_n is packed in 16 bits)
-            atomicAdd(&hist[p[u] >> A.wbits], 1u);
+            bool bad;
+            in[u] = i < end;
+            p[u] = in[u] ? bkt_pos(A, i, bad) : 0u;
         }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t y = __shfl_xor(qm, o), f = __shfl_xor(fl, o);
-        qm = y > qm ? y : qm;
-        fl |= f;
-    }
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = qm, wflag[threadIdx.x >> 6] = fl;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < kBktThreads / 64; ++k) {
-            qm = wmax[k] > qm ? wmax[k] : qm;
-            fl |= wflag[k];
-        }
-        A.bstat[2 * blockIdx.x] = qm;
-        A.bstat[2 * blockIdx.x + 1] = fl;
-    }
     for (int h = threadIdx.x; h < H; h += kBktThreads) A.mat[(int64_t)blockIdx.x * H + h] = hist[h];
 }
 
@@ -515,7 +488,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     __shared__ uint32_t ws[kBktThreads / 64];
     __shared__ uint32_t rq, rf;
     const int H = A.nbkt, nb = A.nblk, b = blockIdx.x;
-    if (threadIdx.x == 0) rq = 0u, rf = 0u;
+    if (threadIdx.x == 0) rq = 0u, rf = 0u;  // the block's largest query length and flags
     const int64_t beg = (int64_t)b * A.chunk;
     const int64_t end = beg + A.chunk < A.n ? beg + A.chunk : A.n;
     // bucket h's total and its reads in blocks before b, from the count rows: wave v takes rows
@@ -557,61 +530,74 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     }
     __syncthreads();
     lds_scan_excl<kBktThreads, kBktMax / kBktThreads>(next, H, ws);
-    if (b == 0) {  // every bucket's first slot; the batch's largest query length and flags
+    if (b == 0) {  // every bucket's first slot, for the rank pass
         for (int h = threadIdx.x; h < H; h += kBktThreads) A.bbase[h] = next[h];
-        uint32_t qm = 0, fl = 0;
-        for (int k = threadIdx.x; k < nb; k += kBktThreads) {
-            qm = A.bstat[2 * k] > qm ? A.bstat[2 * k] : qm;
-            fl |= A.bstat[2 * k + 1];
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t y = __shfl_xor(qm, o), f = __shfl_xor(fl, o);
-            qm = y > qm ? y : qm;
-            fl |= f;
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMax(&rq, qm);
-            atomicOr(&rf, fl);
-        }
-        __syncthreads();  // (uniform: b == 0 for the whole block)
-        if (threadIdx.x == 0) {
-            A.bbase[H] = (uint32_t)A.n;
-            *A.qmax = rq;
-            *A.overflow = bkt_flags(A, rq, rf);
-        }
-        const size_t pad0 = A.cap, pad1 = ((size_t)A.cap + 15) / 16 * 16 + 16;  // seq_event_bytes(cap): zero
-        for (size_t at = pad0 + threadIdx.x; at < pad1; at += kBktThreads) A.o_seq[at] = 0;
+        if (threadIdx.x == 0) A.bbase[H] = (uint32_t)A.n;
     }
     for (int h = threadIdx.x; h < H; h += kBktThreads) next[h] += pre[h];
     __syncthreads();
-    constexpr int B = 8;
+    constexpr int B = 4;  // reads per thread whose loads are in flight together
+    uint32_t qm = 0, fl = 0;
     for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)B * kBktThreads) {
-        uint4 rec[B];
+        uint32_t p[B], cb[B], cn[B], sn[B];
 #pragma unroll
         for (int u = 0; u < B; ++u) {
             const int64_t i = i0 + (int64_t)u * kBktThreads;
-            rec[u] = make_uint4(0u, 0u, 0u, 0u);
+            p[u] = 0u, cb[u] = 0u, cn[u] = 0u, sn[u] = 0u;
             if (i < end) {
                 bool bad;
-                const uint32_t q = A.qlen[i];
-                rec[u] = make_uint4(bkt_pos(A, i, bad), A.cig_beg[i], A.seq_nib[i],
-                                    (A.cig_n[i] & 0xFFFFu) | ((q < kQlenMax ? q : kQlenMax) << 16));
+                p[u] = bkt_pos(A, i, bad);
+                fl |= bad ? 2u : 0u;
+                cb[u] = A.cig_beg[i];
+                cn[u] = A.cig_n[i];
+                sn[u] = A.seq_nib[i];
             }
         }
+        uint32_t w[B][8];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[u][k] = (uint32_t)k < cn[u] ? A.cigar[cb[u] + k] : 0u;
 #pragma unroll
         for (int u = 0; u < B; ++u) {
             const int64_t i = i0 + (int64_t)u * kBktThreads;
             if (i >= end) break;
-            const uint32_t j = atomicAdd(&next[rec[u].x >> A.wbits], 1u);
-            A.brec[j] = rec[u];
+            uint32_t q = 0;  // query length (M/I/=/X)
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (qcons(w[u][k] & 15u)) q += w[u][k] >> 4;
+            for (uint32_t k = 8; k < cn[u]; ++k) {
+                const uint32_t x = A.cigar[cb[u] + k];
+                if (qcons(x & 15u)) q += x >> 4;
+            }
+            qm = q > qm ? q : qm;
+            fl |= cn[u] > 0xFFFFu ? 4u : 0u;  // (cig_n is packed in 16 bits)
+            const uint32_t j = atomicAdd(&next[p[u] >> A.wbits], 1u);
+            A.brec[j] = make_uint4(p[u], cb[u], sn[u], (cn[u] & 0xFFFFu) | ((q < kQlenMax ? q : kQlenMax) << 16));
         }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(qm, o), f = __shfl_xor(fl, o);
+        qm = y > qm ? y : qm;
+        fl |= f;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&rq, qm);
+        atomicOr(&rf, fl);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        A.bstat[2 * b] = rq;
+        A.bstat[2 * b + 1] = rf;
     }
 }
 
 __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     __shared__ uint32_t cnt[kBktLowMax];
     __shared__ uint32_t ws[kRankThreads / 64];
+    __shared__ uint32_t rq, rf;
     const int h = blockIdx.x, t = threadIdx.x;
+    if (t == 0) rq = 0u, rf = 0u;
     const uint32_t bs = A.bbase[h], be = A.bbase[h + 1];
     const int W = 1 << A.wbits;
     const uint32_t lo_mask = (uint32_t)W - 1u;
@@ -620,6 +606,29 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     for (int k = 0; k < kRankRegs; ++k) {
         const uint32_t r = bs + t + k * kRankThreads;
         rec[k] = r < be ? A.brec[r] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (h == 0) {  // the batch's largest query length and flags; the copy's zero padding
+        uint32_t qm = 0, fl = 0;
+        for (int b = t; b < A.nblk; b += kRankThreads) {
+            qm = A.bstat[2 * b] > qm ? A.bstat[2 * b] : qm;
+            fl |= A.bstat[2 * b + 1];
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t y = __shfl_xor(qm, o), f = __shfl_xor(fl, o);
+            qm = y > qm ? y : qm;
+            fl |= f;
+        }
+        if ((t & 63) == 0) {
+            atomicMax(&rq, qm);
+            atomicOr(&rf, fl);
+        }
+        __syncthreads();  // (uniform: h == 0 for the whole block)
+        if (t == 0) {
+            *A.qmax = rq;
+            *A.overflow = bkt_flags(A, rq, rf);
+        }
+        const size_t pad0 = A.cap, pad1 = ((size_t)A.cap + 15) / 16 * 16 + 16;  // seq_event_bytes(cap): zero
+        for (size_t at = pad0 + t; at < pad1; at += kRankThreads) A.o_seq[at] = 0;
     }
     for (int k = t; k < W; k += kRankThreads) cnt[k] = 0u;
     __syncthreads();
@@ -839,7 +848,6 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     hipError_t e = hipSuccess;
     if (!exact && L.bkt.ok && !bkt_off) {
         A.mat = (uint32_t*)(b + L.mat);
-        A.qlen = A.src;
         A.bstat = (uint32_t*)(b + L.bstat);
         A.bbase = (uint32_t*)(b + L.bbase);
         A.brec = A.rec;

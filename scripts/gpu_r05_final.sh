@@ -2,7 +2,7 @@
 # Round 5's closing GPU sessions on the final library, by STAGE:
 #   A  the sort tests and A/B, the unsorted sort's kernel trace, then the profiles of c2 c3 c3q20
 #   B  the profiles of c4 c5, then the default bench line
-#   C  the whole GPU suite and smoke
+#   C  smoke, the whole GPU suite and the default bench line (with the PMC traffic of this library)
 # Every GPU step has its own time limit and the steps are chained: the first failure ends the call.
 set -e -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -20,7 +20,7 @@ case "${STAGE:?STAGE=A|B|C}" in
     timeout -k 10 600 python bench.py > gpurun_out/bench_r05g.log 2>&1
     ;;
   C)
-    STEPS="smoke tests" bash scripts/gpu_round.sh > gpurun_out/final_c.log 2>&1
+    STEPS="smoke tests bench" bash scripts/gpu_round.sh > gpurun_out/final_c.log 2>&1
     grep -q ALLDONE gpurun_out/final_c.log
     ;;
 esac

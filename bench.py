@@ -65,10 +65,12 @@ KERNEL_NAMES = {"pileup": "k_pileup (fused kernel 1 + 2)", "solo": "k_pileup_sol
                 "rc_indexed": "k_rc from a prebuilt device index (run records + chunk summaries of "
                               "k_index_runs, replayed; not the step)",
                 "stats": "k_stats_lane (kernel 2)",
-                "amplicons": "k_amplicon (per amplicon window: integer mean and radix-select median of the "
-                             "coverage, numpy mean and median of both entropies)",
+                "amplicons": "k_amplicon (per amplicon window: integer mean and median of the coverage, numpy "
+                             "mean and median of both entropies; windows of <= 512 positions staged in LDS and "
+                             "sorted by one wave's register bitonic sort, longer ones by radix select)",
                 "index": "k_index_runs + k_index_tiles (the batch's device index, bc_reads_index)",
-                "summary": "summary: k_sum_chunks (last partial buffer of each contig) + k_sum_final (folds, one launch)",
+                "summary": "summary: k_sum_chunks (each contig's 8192-position buffers; a short contig's last "
+                           "partial buffer in the same launch) + k_sum_final (folds, one launch)",
                 "solo_sum": "summary-only kernels 1 + 2, read-parallel (k_sum_reads + k_sum_exact + k_sum_buffers per "
                             "contig; durations summed over the contigs' launches, which overlap on the streams)"}
 

@@ -161,16 +161,20 @@ IMAGE_OK = [[(0, 150)], [(4, 5), (0, 140), (4, 5)], [(0, 70), (2, 2), (0, 78)],
             [(5, 3), (0, 100), (2, 1), (0, 49), (4, 2)]]
 FALLBACK = [[(2, 3), (0, 147)], [(0, 147), (2, 3)], [(0, 50), (2, 2), (0, 50), (2, 2), (0, 46)],
             [(0, 100), (3, 5000), (0, 50)], [(1, 4), (0, 146)]]
+# 2 x 250 bp-style reads: a 256-read chunk's sequence (~32 KB) does not fit k_rc's stage, and
+# every read is longer than a gather slot (such chunks keep the run-table walk)
+LONG250 = [[(0, 250)], [(4, 5), (0, 240), (4, 5)], [(0, 120), (2, 2), (0, 130)], [(0, 100), (1, 2), (0, 148)]]
 
 
-@pytest.mark.parametrize("mix", ["image", "fallback", "mixed"])
+@pytest.mark.parametrize("mix", ["image", "fallback", "mixed", "long250"])
 @pytest.mark.parametrize("mbq,ncols", [(0, 5), (20, 6)])
 def test_rc_event_image_shapes(ctx, mix, mbq, ncols):
     """Deep sorted batches through k_rc: chunks the event image takes, chunks whose reads start
-    or end with a deletion / have 3 runs / span too many windows (run tables), and both mixed."""
+    or end with a deletion / have 3 runs / span too many windows (run tables), both mixed, and
+    deep 250-base reads (chunks too long for the stage and the gather slots)."""
     ctx.set_shape("rc")
-    tpl = {"image": IMAGE_OK, "fallback": FALLBACK, "mixed": IMAGE_OK + FALLBACK[:2]}[mix]
-    rng = np.random.default_rng({"image": 31, "fallback": 32, "mixed": 33}[mix])
+    tpl = {"image": IMAGE_OK, "fallback": FALLBACK, "mixed": IMAGE_OK + FALLBACK[:2], "long250": LONG250}[mix]
+    rng = np.random.default_rng({"image": 31, "fallback": 32, "mixed": 33, "long250": 34}[mix])
     L = 12_000
     b = shaped_batch(rng, L, 40_000, tpl)
     exp, (br, _) = O.bcount(L, mbq, b)

@@ -6,7 +6,7 @@
 // sequence.  An unsorted batch (reads of one reference in any order) is therefore put in start
 // order here, with no host round trip.  The default is the bucketed sort (k_bkt_*, below): no
 // global atomics, per-block LDS histograms of the starts' high bits, one block per bucket sorting
-// by the low bits, the sequence copied in destination order (C3 in random order: 164 -> 98 us).
+// by the low bits, the sequence copied in destination order (C3 in random order: 164 -> 88 us).
 // The counting sort with one global atomic per read (below) remains for references too long for
 // the buckets (more than 2^24 starts) and, with `exact`, for reads of very different lengths:
 //   1. k_sort_count    counting sort by start position: one atomic per read on its position's bin
@@ -393,15 +393,20 @@ __global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
 //                  overflow word;
 //   k_bkt_copy     4 lanes per sorted slot: fields, sequence and qualities into fixed slots, so
 //                  a wave writes whole lines of the copy (destination order).
-// Measured and dropped: rank and copy fused (one block per bucket staging its records in LDS and
+// 256 buckets of ~4,096 reads and 4,096-read blocks (C3: 245 of them, every CU busy) beat 512 buckets
+// and 8,192-read blocks (123 CUs, the scatter's CIGAR decode VALU-bound on them): 88 vs 94 us.
+// Measured and dropped: the scatter's first fields requested before the count rows are summed (no
+// change, 25 us); rank and copy fused (one block per bucket staging its records in LDS and
 // copying them): 79 us against 10 + 53; the matrix scanned by scan_u32 (3 launches, 14 us)
 // instead of each scatter block summing the rows itself.
 constexpr int kBktThreads = 1024;  // count / scatter blocks
 constexpr int kBktGroup = 8;       // scatter: buckets per lane and rows per wave whose count loads
 constexpr int kBktRows = 4;        // are in flight together
-constexpr int kRankThreads = 512;
+constexpr int kRankThreads = 1024;
 constexpr int kRankRegs = 8;       // records per rank thread held in registers
 constexpr int kBktMax = 4096;      // buckets (LDS words of the count / scatter passes)
+constexpr int kBktTarget = 256;    // buckets aimed at (fewer starts per bucket: larger buckets)
+constexpr int kBktChunk = 4096;    // reads per count / scatter block aimed at
 constexpr int kBktLowMax = 4096;   // low-bit bins of one bucket (2^12)
 constexpr uint32_t kQlenMax = 0xFFFFu;  // query lengths packed in 16 bits
 
@@ -737,8 +742,8 @@ __global__ __launch_bounds__(256) void k_bkt_copy(SortArgs A) {
     copy_reads<R>(A, a, jj, ok, sub, slot);
 }
 
-// The bucketed sort's shape: buckets of 2^wbits starts (at most 512 of them, or 4096 of 4096),
-// blocks of `chunk` reads, so that the count rows (blocks x buckets) stay within 65,536 words:
+// The bucketed sort's shape: buckets of 2^wbits starts (at most 256 of them, or 4096 of 4096),
+// blocks of ~4,096 reads, so that the count rows (blocks x buckets) stay within 65,536 words:
 // each scatter block reads them all.  ok = false: the counting sort with global atomics.
 struct BktPlan {
     bool ok;
@@ -751,12 +756,12 @@ BktPlan bkt_plan(const bc_reads& r) {
     const int64_t n = r.n_reads, nbins = r.max_end + 2;
     if (n <= 0 || n >= (int64_t)0xFFFFFFFFll || nbins <= 0) return P;
     int w = 0;
-    while (w < 12 && (nbins + (1ll << w) - 1) >> w > 512) ++w;
+    while (w < 12 && (nbins + (1ll << w) - 1) >> w > kBktTarget) ++w;
     const int64_t H = (nbins + (1ll << w) - 1) >> w;
     if (H > kBktMax) return P;
     P.wbits = w;
     P.nbkt = (int)H;
-    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((n + 8191) / 8192, 65536 / H));
+    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((n + kBktChunk - 1) / kBktChunk, 65536 / H));
     P.chunk = (n + nblk - 1) / nblk;
     P.nblk = (int)((n + P.chunk - 1) / P.chunk);
     P.ok = true;

@@ -247,12 +247,24 @@ int bc_ctx_release_scratch(bc_ctx* c) {
     if (!c) return fail(BC_E_ARG, "ctx is NULL");
     DeviceGuard g(c->device);
     if (c->rc_scratch || c->out_scratch || c->sum_scratch) HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->rc_scratch) HIP_TRY(hipFree(c->rc_scratch));
-    if (c->out_scratch) HIP_TRY(hipFree(c->out_scratch));
-    if (c->sum_scratch) HIP_TRY(hipFree(c->sum_scratch));
+    // one buffer at a time: its pointer and size are cleared whether or not its free succeeded,
+    // so no later call frees it twice; the first error is returned after all three
+    hipError_t first = hipSuccess;
+    const char* where = nullptr;
+    auto drop = [&](void*& p, size_t& bytes, const char* what) {
+        if (p) {
+            const hipError_t e = hipFree(p);
+            if (e != hipSuccess && first == hipSuccess) first = e, where = what;
+        }
+        p = nullptr;
+        bytes = 0;
+    };
+    void* rc = c->rc_scratch;
+    drop(rc, c->rc_scratch_bytes, "hipFree(rc_scratch)");
     c->rc_scratch = nullptr;
-    c->out_scratch = c->sum_scratch = nullptr;
-    c->rc_scratch_bytes = c->out_scratch_bytes = c->sum_scratch_bytes = 0;
+    drop(c->out_scratch, c->out_scratch_bytes, "hipFree(out_scratch)");
+    drop(c->sum_scratch, c->sum_scratch_bytes, "hipFree(sum_scratch)");
+    if (first != hipSuccess) return hip_fail(first, where);
     return BC_OK;
 }
 
@@ -454,26 +466,29 @@ int bc_reads_sort(bc_ctx* c, const bc_reads* r, bc_reads* out, void* d_mem, size
     const size_t need = bc::sort_bytes(*r);
     if (!d_mem || bytes < need) return fail(BC_E_ARG, "bc_reads_sort: d_mem smaller than bc_reads_sort_bytes");
     if ((uintptr_t)d_mem & 255u) return fail(BC_E_ARG, "bc_reads_sort: d_mem must be 256-byte aligned");
+    if (!bc::sort_fits(*r))
+        return fail(BC_E_ARG, "bc_reads_sort: batch too large to sort (seq_bytes + 5 n_reads + 16 > 0x55555550): "
+                              "split it");
     DeviceGuard g(c->device);
     bc_reads tmp;
     {
         Timed tm(c, BC_K_SORT);
         HIP_TRY(bc::launch_sort(c->stream, *r, tmp, d_mem));
     }
-    uint32_t overflow = 0;
-    HIP_TRY(hipMemcpyAsync(&overflow, bc::sort_overflow_word(*r, d_mem), 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (overflow == 4u) {  // reads of very different lengths: the fixed relay slots do not fit
-        {
-            Timed tm(c, BC_K_SORT);
-            HIP_TRY(bc::launch_sort(c->stream, *r, tmp, d_mem, true));
-        }
-        HIP_TRY(hipMemcpyAsync(&overflow, bc::sort_overflow_word(*r, d_mem), 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-    }
-    if (overflow & 2u) return fail(BC_E_ARG, "bc_reads_sort: a read starts outside [0, max_end] (max_end not truthful)");
-    if (overflow) return fail(BC_E_ARG, "bc_reads_sort: the reads' sequences overlap (sorted copy would not fit)");
     *out = tmp;
+    return BC_OK;
+}
+
+int bc_reads_sort_check(bc_ctx* c, const bc_reads* r, const void* d_mem) {
+    if (!c || !r) return fail(BC_E_ARG, "NULL argument");
+    if (r->n_reads <= 0) return BC_OK;
+    if (!d_mem) return fail(BC_E_ARG, "bc_reads_sort_check: d_mem is NULL");
+    DeviceGuard g(c->device);
+    HIP_TRY(hipMemcpyAsync(c->h_err, bc::sort_flags_word(*r, d_mem), 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint32_t flags = (uint32_t)(*c->h_err & 0xFFFFFFFFu);
+    if (flags & 2u) return fail(BC_E_ARG, "bc_reads_sort: a read starts outside [0, max_end] (max_end not truthful)");
+    if (flags & 1u) return fail(BC_E_ARG, "bc_reads_sort: the reads' sequences overlap (sorted copy would not fit)");
     return BC_OK;
 }
 
@@ -620,8 +635,17 @@ int bc_pileup_partials(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, in
                     HIP_TRY(hipMemsetAsync(c->sum_scratch, 0, need, c->stream));
                 }
                 Timed tm(c, BC_K_SOLO);
-                HIP_TRY(bc::launch_sum_sparse(c->stream, *r, L, mbq, k, nf, c->d_err, parts, c->sum_scratch,
-                                                 c->sum_scratch_bytes));
+                const hipError_t e = bc::launch_sum_sparse(c->stream, *r, L, mbq, k, nf, c->d_err, parts,
+                                                           c->sum_scratch, c->sum_scratch_bytes);
+                if (e != hipSuccess) {
+                    // the leaf arrays may be left partly counted (k_sum_buffers re-zeroes them at the
+                    // end of the chain): give them back, so the next call allocates and zeroes afresh
+                    (void)hipStreamSynchronize(c->stream);
+                    (void)hipFree(c->sum_scratch);
+                    c->sum_scratch = nullptr;
+                    c->sum_scratch_bytes = 0;
+                    return hip_fail(e, "bc::launch_sum_sparse");
+                }
             }
 #endif
             if (!parts.fused) return fail(BC_E_ARG, "internal: summary-only sweep without fused partials");

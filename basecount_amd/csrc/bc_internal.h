@@ -92,9 +92,11 @@ hipError_t launch_pileup_tiles(hipStream_t s, const bc_reads& r, int64_t L, int6
                                double* pc, double* ent, double* sec, unsigned long long* d_err, int shape = 0,
                                int tile_waves = 0, SumParts* parts = nullptr);
 // Summary only (main.py:469-499) for a sparse sorted batch: the read-parallel summary (counted
-// positions per 128-position leaf, exact walks of the leaves two reads share, numpy's tree per
-// quarter) into parts' quarter partials and tail arrays; `scratch` (>= sum_sparse_bytes(L) bytes,
-// laid out by its capacity) zeroed when allocated, left zeroed.  Needs L >= kNpBuf.
+// positions per 128-position leaf, exact walks of the leaves two reads share; k_sum_buffers adds
+// each 8192-position buffer's 64 leaves in numpy's tree order) into WHOLE-buffer partials
+// (parts.ent / cov / nz, parts.whole_buffers set: the fold is told so through a header value of
+// 0) and the tail arrays; `scratch` (>= sum_sparse_bytes(L) bytes, laid out by its capacity)
+// zeroed when allocated, left zeroed (on a launch error the caller drops it).  Needs L >= kNpBuf.
 size_t sum_sparse_bytes(int64_t L);
 hipError_t launch_sum_sparse(hipStream_t s, const bc_reads& r, int64_t L, uint32_t mbq, int k, double nf,
                              unsigned long long* d_err, SumParts& parts, void* scratch, size_t scratch_bytes);
@@ -113,13 +115,13 @@ inline bool pileup_is_solo(const bc_reads& r, int64_t L, int shape, int tile_wav
 
 // ---- the coordinate-sorted copy of an unsorted batch (bc_sort.hip) ----
 size_t sort_bytes(const bc_reads& r);
-// enqueues the sort into mem (sort_bytes(r) bytes) and fills `out` (sorted, no index): the relay
-// into fixed slots, or with `exact` the gather, scanned offsets and copy
-hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem, bool exact = false);
-// device word set when the sorted sequence would not fit its buffer (read after a sync): bit 0
-// the exact steps' sequences overlap, bit 1 a start outside [0, max_end], bit 2 the fixed
-// relay slots do not fit (run the exact steps)
-const uint32_t* sort_overflow_word(const bc_reads& r, void* mem);
+// enqueues the sort into mem (sort_bytes(r) bytes; stream-ordered, no host round trip) and fills
+// `out` (sorted, no index); needs sort_fits(r)
+hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem);
+bool sort_fits(const bc_reads& r);
+// device word of caller errors (read after a sync): bit 0 the reads' sequences overlap (the copy
+// did not fit), bit 1 a start outside [0, max_end]
+const uint32_t* sort_flags_word(const bc_reads& r, const void* mem);
 
 // ---- the device index of a sorted batch (bc_index.hip) ----
 // bc_reads.index_tag: the batch identity an index was built for (never 0)

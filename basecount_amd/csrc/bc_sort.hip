@@ -4,30 +4,24 @@
 // (count.cpp:22-97 adds one per event), but the fast kernels do: the tiled k_pileup walks a
 // contiguous range of reads per tile and the read-chunked k_rc stages a chunk's contiguous
 // sequence.  An unsorted batch (reads of one reference in any order) is therefore put in start
-// order here, with no host round trip.  The default is the bucketed sort (k_bkt_*, below): no
-// global atomics, per-block LDS histograms of the starts' high bits, one block per bucket sorting
-// by the low bits, the sequence copied in destination order (C3 in random order: 164 -> 88 us).
-// The counting sort with one global atomic per read (below) remains for references too long for
-// the buckets (more than 2^24 starts) and, with `exact`, for reads of very different lengths:
-//   1. k_sort_count    counting sort by start position: one atomic per read on its position's bin
-//                      (the returned old value is the read's rank inside the bin), the read's
-//                      query length from its CIGAR (M/I/=/X), its fields packed in 32 bytes;
-//   2. scan_u32        exclusive prefix sum of the bins (3 launches: tile sums, their scan, add);
-//   3. k_sort_perm     the permutation (one random 4-byte store per read), then k_sort_gather:
-//                      each sorted slot's fields gathered with coalesced stores, and the bytes of
-//                      sequence it needs (rounded up to whole words);
-//   4. scan_u32        of those bytes: the sorted sequence buffer's offsets;
-//   5. k_sort_seq      each read's aligned sequence (and its qualities) copied word by word to its
-//                      offset, so a chunk of sorted reads has one contiguous sequence segment again.
-// Steps 3 (gather) to 5 are fused into k_sort_relay when they can be: every read gets a slot of
-// the same size (the longest read's bytes, its maximum taken in k_sort_count), so there are no
-// offsets to scan (C3: 103 -> 76 us); a batch whose fixed slots would not fit the copy's buffer
-// (reads of very different lengths) is flagged and sorted again with the exact steps above
-// (bc_reads_sort).  Measured and dropped: one bin per 128-byte line (the count's atomics took as
-// long: 45.8 vs 48.8 us, while the strided scan and permutation got slower), rocPRIM's radix
-// sort of the (start, index) pairs (155 us for C3's 1 M pairs over 15 bits).
-// The CIGAR buffer is shared with the input (reads keep their cig_beg).  HBM traffic ~ 2x the
-// batch's sequence + 40 B per read; every pass is a streaming, fully parallel kernel.
+// order here, with no host round trip: bc_reads_sort only enqueues (stream-ordered, graph-
+// capturable), every decision about the layout is taken on the device.  The default is the
+// bucketed sort (k_bkt_*, below): no global atomics, per-block LDS histograms of the starts' high
+// bits, one block per bucket sorting by the low bits, the sequence copied in destination order.
+// References with more than 2^24 starts take the counting sort (one global atomic per read on its
+// start's bin, k_sort_count + scan_u32 + k_sort_relay).
+//
+// The copy (both sorts): every read gets a slot of the same size, the batch's longest read's
+// bytes, when those slots fit the copy's buffer (T = 1.5 x the batch's bytes); otherwise (reads of
+// very different lengths) the slots shrink to half the batch's mean and a read longer than its
+// slot takes its bytes from a bump allocator past the slots (one global atomic per such read).
+// Either way everything fits T, so there is nothing to fall back to and nothing for the host to
+// wait for.  Caller errors (a start outside [0, max_end], reads whose sequences overlap so the
+// copy overflows) are flagged in a device word (bc_reads_sort_check reads it); the sorted copy is
+// still safe to count (such reads are clamped to start 0 / given no CIGAR).
+// Measured and dropped: one bin per 128-byte line (the count's atomics took as long), rocPRIM's
+// radix sort of the (start, index) pairs (155 us for C3's 1 M pairs over 15 bits); the round-5
+// exact fallback (gather + scanned offsets), which needed a blocking host read of the flags.
 #include "bc_internal.h"
 
 namespace bc {
@@ -135,23 +129,21 @@ struct SortArgs {
     const uint8_t* seq;
     const uint8_t* qual;
     int64_t n;
-    uint32_t* bins;   // [nbins] counts, then offsets
-    uint4* rec;       // [2n] read i: {pos, cig_beg, cig_n, seq_nib}, {qlen, rank in its bin, 0, 0}
-    uint32_t* src;    // [n] source nibble index of sorted read j
-    uint32_t* perm;   // [n] the read at sorted slot j
+    uint32_t* bins;   // [nbins] counts, then offsets (counting sort)
+    uint4* rec;       // counting sort: [2n] read i: {pos, cig_beg, cig_n, seq_nib}, {qlen, rank in its bin, 0, 0}
     int32_t* o_pos;
     uint32_t* o_cig_beg;
     uint32_t* o_cig_n;
     uint32_t* o_seq_nib;
-    uint32_t* o_bytes;  // sequence bytes of sorted read j, then their offsets
-    uint32_t* total;    // sum of o_bytes (device word)
-    uint32_t* overflow; // set when the sorted sequence would not fit cap bytes
+    uint32_t* bump;     // bytes handed out past the fixed slots (device word, zeroed before the copy)
+    uint32_t* overflow; // caller errors: bit 0 the copy overflowed (overlapping sequences), bit 1 a bad start
+    uint32_t* qmax;     // the batch's largest query length (device word)
     uint8_t* o_seq;
     uint8_t* o_qual;
-    uint32_t cap;       // bytes of o_seq (o_qual: twice as many)
+    uint32_t cap;       // the batch's bytes bound: seq_bytes + 5 n + 16 (every read's slot bytes sum to less)
+    uint32_t room;      // bytes of o_seq (o_qual: twice as many): cap + cap / 2
     int64_t qual_bytes;
     int64_t nbins;      // bins: starts in [0, nbins - 1)
-    uint32_t* qmax;     // the batch's largest query length (device word; fast variant)
     // the bucketed variant (k_bkt_*): buckets of 2^wbits starts, nbkt of them; block b of the
     // count and scatter passes takes reads [b * chunk, (b + 1) * chunk)
     uint32_t* mat;      // [nblk][nbkt]: reads of bucket h in block b
@@ -163,13 +155,9 @@ struct SortArgs {
     int nblk, nbkt, wbits;
 };
 
-
-
 // read i: its rank inside its start's bin (one atomic on the bin), its query length from the
-// CIGAR (M/I/=/X), and its fields packed into one 32-byte record (written coalesced), so the
-// gather below reads one 32-byte record per read instead of five scattered 4-byte fields
-// (FIXED: also the batch's largest query length, for k_sort_relay's fixed slots)
-template <bool FIXED>
+// CIGAR (M/I/=/X), and its fields packed into one 32-byte record (written coalesced); the batch's
+// largest query length (one guarded atomic per block)
 __global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
     __shared__ uint32_t wmax[4];
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -177,7 +165,7 @@ __global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
     if (i < A.n) {
         int32_t pos = A.pos[i];
         if (pos < 0 || (int64_t)pos >= A.nbins - 1) {  // a start outside [0, max_end]: the caller's batch is wrong
-            atomicOr(A.overflow, 2u);                     // (bc_reads_sort returns BC_E_ARG)
+            atomicOr(A.overflow, 2u);                     // (bc_reads_sort_check reports it)
             pos = 0;
         }
         const uint32_t cb = A.cig_beg[i], cn = A.cig_n[i], sn = A.seq_nib[i];
@@ -196,99 +184,91 @@ __global__ __launch_bounds__(256) void k_sort_count(SortArgs A) {
         A.rec[2 * i] = make_uint4((uint32_t)pos, cb, cn, sn);
         A.rec[2 * i + 1] = make_uint4(q, rank, 0u, 0u);
     }
-    if (FIXED) {  // the largest query length (one guarded atomic per block: one word's atomics serialize)
-        uint32_t m = q;
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t y = __shfl_xor(m, o);
-            m = y > m ? y : m;
-        }
-        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t a = wmax[0] > wmax[1] ? wmax[0] : wmax[1], b = wmax[2] > wmax[3] ? wmax[2] : wmax[3];
-            const uint32_t bm = a > b ? a : b;
-            if (bm > __hip_atomic_load(A.qmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(A.qmax, bm);
-        }
+    uint32_t m = q;
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(m, o);
+        m = y > m ? y : m;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t a = wmax[0] > wmax[1] ? wmax[0] : wmax[1], b = wmax[2] > wmax[3] ? wmax[2] : wmax[3];
+        const uint32_t bm = a > b ? a : b;
+        if (bm > __hip_atomic_load(A.qmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(A.qmax, bm);
     }
 }
 
-__global__ __launch_bounds__(256) void k_sort_perm(SortArgs A) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= A.n) return;
-    const uint4 a = A.rec[2 * i], b = A.rec[2 * i + 1];
-    A.perm[A.bins[a.x] + b.y] = (uint32_t)i;
+// bytes of a read's copy: its aligned bases at its nibble parity, rounded up to whole words
+__device__ __forceinline__ uint32_t read_words(uint32_t sn, uint32_t q) { return ((((sn & 1u) + q + 1u) >> 1) + 3u) >> 2; }
+
+// The copy's slot size, the same in every thread: the longest read's bytes (at either nibble
+// parity, in words) when n such slots fit the buffer -- then no read is longer than its slot --
+// else half the batch's mean bytes per read, n slots taking at most cap / 2 and the longer reads
+// at most cap (their bytes sum to less) from the bump allocator past them: room = 1.5 cap.
+__device__ __forceinline__ uint32_t copy_slot(const SortArgs& A, uint32_t qmax) {
+    const uint64_t full = (((uint64_t)qmax + 2u) / 2u + 3u) & ~3ull;
+    if (full * (uint64_t)A.n <= (uint64_t)A.room) return (uint32_t)full;
+    return (uint32_t)(((uint64_t)A.cap / (2u * (uint64_t)A.n)) & ~3ull);
 }
 
-// bytes of a relay slot: the largest read's aligned bases at either nibble parity, in words
-__device__ __forceinline__ uint32_t relay_slot(uint32_t qmax) { return ((qmax + 2u) / 2u + 3u) & ~3u; }
-
-// Reads i in SOURCE order (4 lanes per read, kRelayReads consecutive reads per lane group, their
-// loads batched so each lane has many in flight): read i's 32-byte record (coalesced), its sorted
-// slot j = scanned bin of its start + its rank in the bin (no permutation array), its fields
-// written to slot j, its sequence bytes copied word by word (two aligned source words and a funnel
-// shift; the source is read up to 3 bytes past the read, inside the padded buffer: consecutive
-// reads' bytes are adjacent, so the loads stream) into slot j of the copy, its qualities likewise.
-// The new nibble index keeps the old one's parity.  Bytes of a slot past its read are never read.
-constexpr int kRelayReads = 4;
+// R sorted reads per 4-lane group (lane `sub` of the group): read r has start pos[r], CIGAR
+// (cb[r], cn[r]), source nibble index sn[r], query length q[r] and sorted slot jj[r] (ok[r]:
+// uniform in the group).  Its destination: slot jj[r] of the fixed slots, or (longer than a slot)
+// bytes from the bump allocator; a destination past the buffer (the caller's reads overlap) is
+// flagged and the read written with no CIGAR.  Fields (lane r & 3 writes read r's), the aligned
+// sequence (two source words and a funnel shift per output word; every source word of the
+// unrolled part requested first) and the qualities; the new nibble index keeps the old parity.
 constexpr int kRelayWords = 5;  // words per lane per read in the unrolled part (20 per read: 160 bases)
-__global__ __launch_bounds__(256) void k_sort_relay(SortArgs A) {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t sub = (uint32_t)g & 3u;
-    const int64_t j0 = (g >> 2) * kRelayReads;
-    if (j0 >= A.n) return;
-    const uint32_t slot = relay_slot(*A.qmax);
-    if ((uint64_t)slot * (uint64_t)A.n > (uint64_t)A.cap) {  // the exact steps run instead
-        if (g == 0) atomicOr(A.overflow, 4u);
-        return;
-    }
-    uint4 a[kRelayReads];
-    uint32_t q[kRelayReads], jj[kRelayReads];
+template <int R>
+__device__ __forceinline__ void copy_reads(const SortArgs& A, const uint32_t (&pos)[R], const uint32_t (&cb)[R],
+                                           const uint32_t (&cn)[R], const uint32_t (&sn)[R], const uint32_t (&q)[R],
+                                           const uint32_t (&jj)[R], const bool (&ok)[R], uint32_t sub, uint32_t slot) {
+    uint32_t dst[R];
+    bool keep[R];
 #pragma unroll
-    for (int r = 0; r < kRelayReads; ++r) {
-        const size_t i = (size_t)(j0 + r < A.n ? j0 + r : j0);  // source read
-        a[r] = A.rec[2 * i];  // {pos, cig_beg, cig_n, seq_nib}
-        const uint4 b = A.rec[2 * i + 1];  // {qlen, rank}
-        q[r] = b.x;
-        jj[r] = b.y;
-    }
-#pragma unroll
-    for (int r = 0; r < kRelayReads; ++r) jj[r] += A.bins[a[r].x];  // the read's sorted slot
-    {  // lane `sub` writes read j0 + sub's fields
-        uint4 me = a[0];
-#pragma unroll
-        for (int r = 1; r < kRelayReads; ++r)
-            if (sub == (uint32_t)r) me = a[r];
-        uint32_t mj = jj[0];
-#pragma unroll
-        for (int r = 1; r < kRelayReads; ++r)
-            if (sub == (uint32_t)r) mj = jj[r];
-        if (j0 + sub < A.n) {
-            const uint32_t j = mj;
-            A.o_pos[j] = (int32_t)me.x;
-            A.o_cig_beg[j] = me.y;
-            A.o_cig_n[j] = me.z;
-            A.o_seq_nib[j] = 2u * (slot * (uint32_t)j) + (me.w & 1u);
+    for (int r = 0; r < R; ++r) {
+        const uint32_t bytes = 4u * read_words(sn[r], q[r]);
+        dst[r] = slot * jj[r];
+        keep[r] = true;
+        if (ok[r] && bytes > slot) {  // (uniform in the lane group; only when the slots were shrunk)
+            uint32_t at = 0;
+            if (sub == 0) at = atomicAdd(A.bump, bytes);
+            at = __shfl(at, 0, 4);
+            const uint64_t end = (uint64_t)slot * (uint64_t)A.n + at + bytes;
+            dst[r] = slot * (uint32_t)A.n + at;
+            if (end > (uint64_t)A.room) {  // the reads' bytes exceed cap: overlapping sequences
+                keep[r] = false;
+                if (sub == 0) atomicOr(A.overflow, 1u);
+            }
         }
     }
-    uint32_t x[kRelayReads][kRelayWords + 1];
 #pragma unroll
-    for (int r = 0; r < kRelayReads; ++r) {  // every source word of the unrolled part requested first
-        const uint32_t sn = a[r].w, words = ((((sn & 1u) + q[r] + 1u) >> 1) + 3u) >> 2;
-        const uint32_t* s32 = (const uint32_t*)(A.seq + ((sn >> 1) & ~3u));
+    for (int r = 0; r < R; ++r)
+        if (ok[r] && sub == ((uint32_t)r & 3u)) {
+            const uint32_t j = jj[r];
+            A.o_pos[j] = (int32_t)pos[r];
+            A.o_cig_beg[j] = cb[r];
+            A.o_cig_n[j] = keep[r] ? cn[r] : 0u;
+            A.o_seq_nib[j] = keep[r] ? 2u * dst[r] + (sn[r] & 1u) : 0u;
+        }
+    uint32_t x[R][kRelayWords + 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t words = read_words(sn[r], q[r]);
+        const uint32_t* s32 = (const uint32_t*)(A.seq + ((sn[r] >> 1) & ~3u));
 #pragma unroll
         for (int k = 0; k <= kRelayWords; ++k) {
-            const uint32_t w = sub + 4u * (uint32_t)k;  // the group's lanes read consecutive words
-            x[r][k] = (j0 + r < A.n && w <= words) ? s32[w] : 0u;  // (word `words`: the last shift's upper half)
+            const uint32_t w = sub + 4u * (uint32_t)k;
+            x[r][k] = (ok[r] && keep[r] && w <= words) ? s32[w] : 0u;  // (word `words`: the last shift's upper half)
         }
     }
 #pragma unroll
-    for (int r = 0; r < kRelayReads; ++r) {
-        if (j0 + r >= A.n) break;  // (uniform in the lane group)
-        const uint32_t j = jj[r];
-        const uint32_t sn = a[r].w, from = sn >> 1, words = ((((sn & 1u) + q[r] + 1u) >> 1) + 3u) >> 2;
+    for (int r = 0; r < R; ++r) {
+        if (!ok[r] || !keep[r]) continue;  // (uniform in the lane group)
+        const uint32_t from = sn[r] >> 1, words = read_words(sn[r], q[r]);
         const uint32_t sh = (from & 3u) * 8u;
         const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
-        uint32_t* d32 = (uint32_t*)(A.o_seq + slot * (uint32_t)j);
+        uint32_t* d32 = (uint32_t*)(A.o_seq + dst[r]);
         // word w needs source words w and w + 1: w + 1 is the next lane's (lane 3: lane 0's next)
 #pragma unroll
         for (int k = 0; k < kRelayWords; ++k) {
@@ -302,7 +282,7 @@ __global__ __launch_bounds__(256) void k_sort_relay(SortArgs A) {
             const uint64_t qf = 2 * (uint64_t)from;
             const uint32_t* q32 = (const uint32_t*)(A.qual + (qf & ~3ull));
             const uint32_t qsh = (uint32_t)(qf & 3u) * 8u;
-            uint32_t* dq = (uint32_t*)(A.o_qual + 2 * (uint64_t)slot * (uint64_t)j);
+            uint32_t* dq = (uint32_t*)(A.o_qual + 2 * (uint64_t)dst[r]);
             const uint64_t q0 = qf & ~3ull;
             for (uint32_t w = sub; w < 2 * words; w += 4) {
                 if (q0 + 4ull * w + 8 <= (uint64_t)A.qual_bytes) {
@@ -320,61 +300,28 @@ __global__ __launch_bounds__(256) void k_sort_relay(SortArgs A) {
     }
 }
 
-// sorted read j = read perm[j]: its record gathered (one random 32-byte read), its fields
-// written coalesced, with the bytes of sequence it will take (a multiple of 4, so every output
-// word belongs to one read)
-__global__ __launch_bounds__(256) void k_sort_gather(SortArgs A) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= A.n) return;
-    const uint32_t i = A.perm[j];
-    const uint4 a = A.rec[2 * (size_t)i], b = A.rec[2 * (size_t)i + 1];
-    A.o_pos[j] = (int32_t)a.x;
-    A.o_cig_beg[j] = a.y;
-    A.o_cig_n[j] = a.z;
-    A.src[j] = a.w;
-    A.o_bytes[j] = (((a.w & 1u) + b.x + 1u) / 2u + 3u) & ~3u;
-}
-
-// 16 lanes per sorted read, one 4-byte word each: the read's bytes from its source offset
-// (any alignment: two aligned source words and a funnel shift) to its 4-aligned offset, and the
-// two quality bytes of each; the new nibble index keeps the old one's parity.  The source is
-// read up to 3 bytes past the read (the padded buffers allow it): those bytes land in the read's
-// own padding, which no kernel reads (every walk masks to the read's aligned bases).
-__global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
-    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
-    const uint32_t sub = threadIdx.x & 15u;
-    if (j >= A.n) return;
-    const uint32_t sn = A.src[j], off = A.o_bytes[j];
-    const uint32_t end = j + 1 < A.n ? A.o_bytes[j + 1] : *A.total;
-    if ((uint64_t)end > (uint64_t)A.cap || end < off) {
-        if (sub == 0) atomicOr(A.overflow, 1u);
-        return;
+// Counting sort's copy: reads i in SOURCE order (4 lanes per read, kRelayReads consecutive reads
+// per lane group, their loads batched), read i's 32-byte record (coalesced), its sorted slot j =
+// scanned bin of its start + its rank in the bin (no permutation array), then copy_reads.
+constexpr int kRelayReads = 4;
+__global__ __launch_bounds__(256) void k_sort_relay(SortArgs A) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t sub = (uint32_t)g & 3u;
+    const int64_t j0 = (g >> 2) * kRelayReads;
+    if (j0 >= A.n) return;
+    const uint32_t slot = copy_slot(A, *A.qmax);
+    uint32_t pos[kRelayReads], cb[kRelayReads], cn[kRelayReads], sn[kRelayReads], q[kRelayReads], jj[kRelayReads];
+    bool ok[kRelayReads];
+#pragma unroll
+    for (int r = 0; r < kRelayReads; ++r) {
+        ok[r] = j0 + r < A.n;
+        const size_t i = (size_t)(ok[r] ? j0 + r : j0);  // source read
+        const uint4 a = A.rec[2 * i], b = A.rec[2 * i + 1];  // {pos, cig_beg, cig_n, seq_nib}, {qlen, rank}
+        pos[r] = a.x, cb[r] = a.y, cn[r] = a.z, sn[r] = a.w, q[r] = b.x, jj[r] = b.y;
     }
-    const uint32_t from = sn >> 1, words = (end - off) >> 2;
-    const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
-    const uint32_t sh = (from & 3u) * 8u;
-    uint32_t* d32 = (uint32_t*)(A.o_seq + off);
-    for (uint32_t w = sub; w < words; w += 16) d32[w] = __builtin_amdgcn_alignbit(s32[w + 1], s32[w], sh);
-    if (A.qual) {
-        const uint64_t qf = 2 * (uint64_t)from;
-        const uint32_t* q32 = (const uint32_t*)(A.qual + (qf & ~3ull));
-        const uint32_t qsh = (uint32_t)(qf & 3u) * 8u;
-        uint32_t* dq = (uint32_t*)(A.o_qual + 2 * (uint64_t)off);
-        const uint64_t q0 = qf & ~3ull;
-        for (uint32_t w = sub; w < 2 * words; w += 16) {
-            if (q0 + 4ull * w + 8 <= (uint64_t)A.qual_bytes) {
-                dq[w] = __builtin_amdgcn_alignbit(q32[w + 1], q32[w], qsh);
-            } else {  // the buffer's last bytes (the quality buffer has no padding)
-                uint32_t v = 0;
-                for (uint32_t bb = 0; bb < 4; ++bb) {
-                    const uint64_t at = qf + 4ull * w + bb;
-                    if (at < (uint64_t)A.qual_bytes) v |= (uint32_t)A.qual[at] << (8 * bb);
-                }
-                dq[w] = v;
-            }
-        }
-    }
-    if (sub == 0) A.o_seq_nib[j] = 2 * off + (sn & 1u);
+#pragma unroll
+    for (int r = 0; r < kRelayReads; ++r) jj[r] += A.bins[pos[r]];  // the read's sorted slot
+    copy_reads<kRelayReads>(A, pos, cb, cn, sn, q, jj, ok, sub, slot);
 }
 
 // ---- the bucketed sort (no global atomics): starts binned by their high bits with per-block
@@ -385,14 +332,16 @@ __global__ __launch_bounds__(256) void k_sort_seq(SortArgs A) {
 //   k_bkt_scatter  block b: every bucket's total and the count of blocks before b from the rows
 //                  (coalesced, L2-resident), their scan in LDS, then each read's slot in (bucket,
 //                  block) from an LDS atomic with return; its 16-byte record (with the query
-//                  length from its CIGAR) written there; the block's largest query length and
-//                  flags; block 0 also writes every bucket's first slot;
+//                  length from its CIGAR) written there (a read whose CIGAR count or query
+//                  length does not fit 16 bits: its source index instead, re-read by the copy);
+//                  the block's largest query length and flags; block 0 also writes every
+//                  bucket's first slot;
 //   k_bkt_rank     one block per bucket, the bucket's records in registers: LDS counting sort by
 //                  the low bits (histogram, scan, ranks), the records written in start order;
 //                  block 0 folds the block stats into the batch's largest query length and the
-//                  overflow word;
-//   k_bkt_copy     4 lanes per sorted slot: fields, sequence and qualities into fixed slots, so
-//                  a wave writes whole lines of the copy (destination order).
+//                  flags word, and zeroes the bump allocator;
+//   k_bkt_copy     4 lanes per sorted slot: fields, sequence and qualities (copy_reads: fixed
+//                  slots, so a wave writes whole lines of the copy, in destination order).
 // 256 buckets of ~4,096 reads and 4,096-read blocks (C3: 245 of them, every CU busy) beat 512 buckets
 // and 8,192-read blocks (123 CUs, the scatter's CIGAR decode VALU-bound on them): 88 vs 94 us.
 // Measured and dropped: the scatter's first fields requested before the count rows are summed (no
@@ -409,6 +358,8 @@ constexpr int kBktTarget = 256;    // buckets aimed at (fewer starts per bucket:
 constexpr int kBktChunk = 4096;    // reads per count / scatter block aimed at
 constexpr int kBktLowMax = 4096;   // low-bit bins of one bucket (2^12)
 constexpr uint32_t kQlenMax = 0xFFFFu;  // query lengths packed in 16 bits
+constexpr int64_t kSortCapMax = 0x55555550;  // room = 1.5 cap < 2^31: nibble indices 2 * room fit 32 bits
+constexpr uint32_t kBigRec = 0xFFFFFFFFu;  // record word 3 of a read whose fields need 32 bits: word 2 = its index
 
 __device__ __forceinline__ uint32_t bkt_pos(const SortArgs& A, int64_t i, bool& bad) {
     int32_t p = A.pos[i];
@@ -480,12 +431,6 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(SortArgs A) {
     }
     __syncthreads();
     for (int h = threadIdx.x; h < H; h += kBktThreads) A.mat[(int64_t)blockIdx.x * H + h] = hist[h];
-}
-
-// slot bytes of the fixed-slot copy (relay_slot) and whether they fit: the flags of the batch
-__device__ __forceinline__ uint32_t bkt_flags(const SortArgs& A, uint32_t qm, uint32_t fl) {
-    if (qm >= kQlenMax || (uint64_t)relay_slot(qm) * (uint64_t)A.n > (uint64_t)A.cap) fl |= 4u;
-    return fl;
 }
 
 __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
@@ -576,9 +521,11 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
                 if (qcons(x & 15u)) q += x >> 4;
             }
             qm = q > qm ? q : qm;
-            fl |= cn[u] > 0xFFFFu ? 4u : 0u;  // (cig_n is packed in 16 bits)
             const uint32_t j = atomicAdd(&next[p[u] >> A.wbits], 1u);
-            A.brec[j] = make_uint4(p[u], cb[u], sn[u], (cn[u] & 0xFFFFu) | ((q < kQlenMax ? q : kQlenMax) << 16));
+            // cig_n and the query length packed in 16 bits each; a read that needs more (only a
+            // caller's batch: BAM's n_cigar_op is 16 bits) keeps its source index for the copy
+            const bool small = cn[u] <= 0xFFFFu && q < kQlenMax;
+            A.brec[j] = make_uint4(p[u], cb[u], small ? sn[u] : (uint32_t)i, small ? cn[u] | q << 16 : kBigRec);
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -630,9 +577,10 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
         __syncthreads();  // (uniform: h == 0 for the whole block)
         if (t == 0) {
             *A.qmax = rq;
-            *A.overflow = bkt_flags(A, rq, rf);
+            *A.overflow = rf;  // (bit 1: a bad start; the copy may add bit 0)
+            *A.bump = 0u;
         }
-        const size_t pad0 = A.cap, pad1 = ((size_t)A.cap + 15) / 16 * 16 + 16;  // seq_event_bytes(cap): zero
+        const size_t pad0 = A.room, pad1 = ((size_t)A.room + 15) / 16 * 16 + 16;  // seq_event_bytes(room): zero
         for (size_t at = pad0 + t; at < pad1; at += kRankThreads) A.o_seq[at] = 0;
     }
     for (int k = t; k < W; k += kRankThreads) cnt[k] = 0u;
@@ -653,93 +601,40 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     }
 }
 
-// R sorted reads per 4-lane group (lane `sub` of the group): read r = record a[r] for slot jj[r]
-// (ok[r]: uniform in the group).  Fields (lane r & 3 writes read r's), the aligned sequence into
-// fixed slots (two source words and a funnel shift per output word; every source word of the
-// unrolled part requested first) and the qualities; the new nibble index keeps the old parity.
-template <int R>
-__device__ __forceinline__ void copy_reads(const SortArgs& A, const uint4 (&a)[R], const uint32_t (&jj)[R],
-                                           const bool (&ok)[R], uint32_t sub, uint32_t slot) {
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (ok[r] && sub == ((uint32_t)r & 3u)) {
-            const uint32_t j = jj[r];
-            A.o_pos[j] = (int32_t)a[r].x;
-            A.o_cig_beg[j] = a[r].y;
-            A.o_cig_n[j] = a[r].w & 0xFFFFu;
-            A.o_seq_nib[j] = 2u * (slot * j) + (a[r].z & 1u);
-        }
-    uint32_t x[R][kRelayWords + 1];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t sn = a[r].z, words = ((((sn & 1u) + (a[r].w >> 16) + 1u) >> 1) + 3u) >> 2;
-        const uint32_t* s32 = (const uint32_t*)(A.seq + ((sn >> 1) & ~3u));
-#pragma unroll
-        for (int k = 0; k <= kRelayWords; ++k) {
-            const uint32_t w = sub + 4u * (uint32_t)k;
-            x[r][k] = (ok[r] && w <= words) ? s32[w] : 0u;  // (word `words`: the last shift's upper half)
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (!ok[r]) continue;  // (uniform in the lane group)
-        const uint32_t j = jj[r];
-        const uint32_t sn = a[r].z, from = sn >> 1, words = ((((sn & 1u) + (a[r].w >> 16) + 1u) >> 1) + 3u) >> 2;
-        const uint32_t sh = (from & 3u) * 8u;
-        const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
-        uint32_t* d32 = (uint32_t*)(A.o_seq + slot * j);
-#pragma unroll
-        for (int k = 0; k < kRelayWords; ++k) {
-            const uint32_t w = sub + 4u * (uint32_t)k;
-            const uint32_t nxt = __shfl_down(x[r][k], 1, 4), wrap = __shfl(x[r][k + 1], 0, 4);
-            if (w < words) d32[w] = __builtin_amdgcn_alignbit(sub == 3u ? wrap : nxt, x[r][k], sh);
-        }
-        for (uint32_t w = sub + 4u * kRelayWords; w < words; w += 4)
-            d32[w] = __builtin_amdgcn_alignbit(s32[w + 1], s32[w], sh);
-        if (A.qual) {
-            const uint64_t qf = 2 * (uint64_t)from;
-            const uint32_t* q32 = (const uint32_t*)(A.qual + (qf & ~3ull));
-            const uint32_t qsh = (uint32_t)(qf & 3u) * 8u;
-            uint32_t* dq = (uint32_t*)(A.o_qual + 2 * (uint64_t)slot * (uint64_t)j);
-            const uint64_t q0 = qf & ~3ull;
-            for (uint32_t w = sub; w < 2 * words; w += 4) {
-                if (q0 + 4ull * w + 8 <= (uint64_t)A.qual_bytes) {
-                    dq[w] = __builtin_amdgcn_alignbit(q32[w + 1], q32[w], qsh);
-                } else {  // the buffer's last bytes (the quality buffer has no padding)
-                    uint32_t v = 0;
-                    for (uint32_t bb = 0; bb < 4; ++bb) {
-                        const uint64_t at = qf + 4ull * w + bb;
-                        if (at < (uint64_t)A.qual_bytes) v |= (uint32_t)A.qual[at] << (8 * bb);
-                    }
-                    dq[w] = v;
-                }
-            }
-        }
-    }
-}
-
-// 4 lanes per sorted slot, R slots per lane group, over every slot (after k_bkt_rank; R = 1)
+// 4 lanes per sorted slot, R slots per lane group, over every slot (after k_bkt_rank; R = 1):
+// the start-ordered records unpacked (a read with 32-bit fields re-read from the source arrays,
+// its query length from its CIGAR) and copied by copy_reads
 template <int R>
 __global__ __launch_bounds__(256) void k_bkt_copy(SortArgs A) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t sub = (uint32_t)g & 3u;
     // a wave's 16 lane groups take 16 R consecutive slots: group q of the wave, step r -> slot
     // base + 16 r + q, so each store instruction writes 16 neighbouring slots
-    const int64_t wbase = (g >> 6) * 16 * R, q = (g & 63) >> 2;
+    const int64_t wbase = (g >> 6) * 16 * R, qg = (g & 63) >> 2;
     if (wbase >= A.n) return;
-    if (*A.overflow & 6u) return;  // bad starts / slots that do not fit: the caller runs the exact steps
-    const uint32_t slot = relay_slot(*A.qmax);
-    uint4 a[R];
-    uint32_t jj[R];
+    const uint32_t slot = copy_slot(A, *A.qmax);
+    uint32_t pos[R], cb[R], cn[R], sn[R], q[R], jj[R];
     bool ok[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int64_t j = wbase + 16 * r + q;
+        const int64_t j = wbase + 16 * r + qg;
         ok[r] = j < A.n;
         jj[r] = (uint32_t)j;
-        a[r] = ok[r] ? A.srec[j] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 a = ok[r] ? A.srec[j] : make_uint4(0u, 0u, 0u, 0u);
+        pos[r] = a.x, cb[r] = a.y, sn[r] = a.z, cn[r] = a.w & 0xFFFFu, q[r] = a.w >> 16;
+        if (a.w == kBigRec) {  // (rare: uniform in the lane group)
+            const uint32_t i = a.z;
+            sn[r] = A.seq_nib[i];
+            cn[r] = A.cig_n[i];
+            uint32_t qq = 0;
+            for (uint32_t k = 0; k < cn[r]; ++k) {
+                const uint32_t x = A.cigar[cb[r] + k];
+                if (qcons(x & 15u)) qq += x >> 4;
+            }
+            q[r] = qq;
+        }
     }
-    copy_reads<R>(A, a, jj, ok, sub, slot);
+    copy_reads<R>(A, pos, cb, cn, sn, q, jj, ok, sub, slot);
 }
 
 // The bucketed sort's shape: buckets of 2^wbits starts (at most 256 of them, or 4096 of 4096),
@@ -769,9 +664,9 @@ BktPlan bkt_plan(const bc_reads& r) {
 }
 
 struct SortLayout {
-    size_t bins, rec, src, perm, o_pos, o_cb, o_cn, o_sn, o_bytes, tmp, words, o_seq, o_qual, mat, bstat, bbase, total;
+    size_t bins, rec, o_pos, o_cb, o_cn, o_sn, tmp, words, o_seq, o_qual, mat, bstat, bbase, total;
     int64_t nbins;
-    uint32_t cap;
+    uint32_t cap, room;
     BktPlan bkt;
 };
 
@@ -781,27 +676,26 @@ SortLayout sort_layout(const bc_reads& r) {
     L.bkt = bkt_plan(r);
     const int64_t mat_words = L.bkt.ok ? (int64_t)L.bkt.nbkt * L.bkt.nblk : 0;
     L.nbins = r.max_end + 2;  // every start <= max_end
-    // every read takes its aligned bases' bytes rounded up to 4 (+ 1 for an odd start)
-    L.cap = (uint32_t)std::min<int64_t>(r.seq_bytes + 5 * n + 16, 0xFFFFFFF0ll);
+    // every read takes its aligned bases' bytes rounded up to 4 (+ 1 for an odd start); the copy's
+    // buffer has half as much again (copy_slot), nibble indices stay below 2^32 (sort_fits)
+    L.cap = (uint32_t)std::min<int64_t>(r.seq_bytes + 5 * n + 16, kSortCapMax);
+    L.room = (uint32_t)((L.cap + L.cap / 2 + 15) / 16 * 16);
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t at = off;
         off += (bytes + 255) / 256 * 256;
         return at;
     };
-    L.bins = take(4 * (size_t)L.nbins);
+    L.bins = L.bkt.ok ? 0 : take(4 * (size_t)L.nbins);
     L.rec = take(32 * (size_t)n);
-    L.src = take(4 * (size_t)n);
-    L.perm = take(4 * (size_t)n);
     L.o_pos = take(4 * (size_t)n);
     L.o_cb = take(4 * (size_t)n);
     L.o_cn = take(4 * (size_t)n);
     L.o_sn = take(4 * (size_t)n);
-    L.o_bytes = take(4 * (size_t)n + 4);
-    L.tmp = take(4 * scan_tmp_words(std::max<int64_t>(L.nbins, n)));
-    L.words = take(16);  // total, overflow
-    L.o_seq = take(seq_event_bytes(L.cap));
-    L.o_qual = r.qual ? take(2 * (size_t)L.cap + 32) : 0;
+    L.tmp = L.bkt.ok ? 0 : take(4 * scan_tmp_words(L.nbins));
+    L.words = take(16);  // bump, flags, qmax
+    L.o_seq = take(seq_event_bytes(L.room));
+    L.o_qual = r.qual ? take(2 * (size_t)L.room + 32) : 0;
     L.mat = take(4 * (size_t)mat_words);
     L.bstat = take(8 * (size_t)(L.bkt.ok ? L.bkt.nblk : 0));
     L.bbase = take(4 * (size_t)(L.bkt.ok ? L.bkt.nbkt + 1 : 0));
@@ -816,10 +710,12 @@ size_t sort_bytes(const bc_reads& r) {
     return sort_layout(r).total;
 }
 
-hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem, bool exact) {
+bool sort_fits(const bc_reads& r) { return r.seq_bytes + 5 * r.n_reads + 16 <= kSortCapMax; }
+
+hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem) {
     const SortLayout L = sort_layout(r);
     uint8_t* b = (uint8_t*)mem;
-    SortArgs A;
+    SortArgs A{};
     A.pos = r.pos;
     A.cig_beg = r.cig_beg;
     A.cig_n = r.cig_n;
@@ -828,31 +724,23 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     A.seq = r.seq;
     A.qual = r.qual;
     A.n = r.n_reads;
-    A.bins = (uint32_t*)(b + L.bins);
     A.rec = (uint4*)(b + L.rec);
-    A.src = (uint32_t*)(b + L.src);
-    A.perm = (uint32_t*)(b + L.perm);
     A.o_pos = (int32_t*)(b + L.o_pos);
     A.o_cig_beg = (uint32_t*)(b + L.o_cb);
     A.o_cig_n = (uint32_t*)(b + L.o_cn);
     A.o_seq_nib = (uint32_t*)(b + L.o_sn);
-    A.o_bytes = (uint32_t*)(b + L.o_bytes);
-    A.total = (uint32_t*)(b + L.words);
-    A.overflow = A.total + 1;
+    A.bump = (uint32_t*)(b + L.words);
+    A.overflow = A.bump + 1;
+    A.qmax = A.bump + 2;
     A.o_seq = b + L.o_seq;
     A.o_qual = r.qual ? b + L.o_qual : nullptr;
     A.cap = L.cap;
+    A.room = L.room;
     A.qual_bytes = r.qual ? r.qual_bytes : 0;
     A.nbins = L.nbins;
-    A.qmax = A.total + 2;
-    uint32_t* tmp = (uint32_t*)(b + L.tmp);
     const unsigned blocks = (unsigned)((r.n_reads + 255) / 256);
-    static const bool bkt_off = [] {  // diagnostic A/B: BC_SORT_BKT=0 runs the global-atomic count
-        const char* v = std::getenv("BC_SORT_BKT");
-        return v && v[0] == '0';
-    }();
     hipError_t e = hipSuccess;
-    if (!exact && L.bkt.ok && !bkt_off) {
+    if (L.bkt.ok) {
         A.mat = (uint32_t*)(b + L.mat);
         A.bstat = (uint32_t*)(b + L.bstat);
         A.bbase = (uint32_t*)(b + L.bbase);
@@ -868,24 +756,18 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
         // one slot per lane group (a wave: 16 slots): 93 us against 95 / 98 / 101 at 2 / 4 / 8
         const int64_t waves = (r.n_reads + 15) / 16;
         hipLaunchKernelGGL(k_bkt_copy<1>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, A);
-    } else {
+    } else {  // more than 2^24 starts: the counting sort with one global atomic per read
+        A.bins = (uint32_t*)(b + L.bins);
+        uint32_t* tmp = (uint32_t*)(b + L.tmp);
         e = hipMemsetAsync(A.bins, 0, 4 * (size_t)L.nbins, s);
-        if (e == hipSuccess) e = hipMemsetAsync(A.total, 0, 16, s);  // total, overflow, qmax
-        // the sorted sequence's padding past cap (BC_SEQ_EVENT) is zero
-        if (e == hipSuccess) e = hipMemsetAsync(A.o_seq + L.cap, 0, seq_event_bytes(L.cap) - L.cap, s);
+        if (e == hipSuccess) e = hipMemsetAsync(A.bump, 0, 16, s);  // bump, flags, qmax
+        // the sorted sequence's padding past room (BC_SEQ_EVENT) is zero
+        if (e == hipSuccess) e = hipMemsetAsync(A.o_seq + L.room, 0, seq_event_bytes(L.room) - L.room, s);
         if (e != hipSuccess) return e;
-        if (exact) hipLaunchKernelGGL(k_sort_count<false>, dim3(blocks), dim3(256), 0, s, A);
-        else hipLaunchKernelGGL(k_sort_count<true>, dim3(blocks), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_sort_count, dim3(blocks), dim3(256), 0, s, A);
         if ((e = scan_u32(s, A.bins, L.nbins, tmp, nullptr)) != hipSuccess) return e;
-        if (exact) hipLaunchKernelGGL(k_sort_perm, dim3(blocks), dim3(256), 0, s, A);
-        if (!exact) {
-            const int64_t groups = (r.n_reads + kRelayReads - 1) / kRelayReads;
-            hipLaunchKernelGGL(k_sort_relay, dim3((unsigned)((groups * 4 + 255) / 256)), dim3(256), 0, s, A);
-        } else {
-            hipLaunchKernelGGL(k_sort_gather, dim3(blocks), dim3(256), 0, s, A);
-            if ((e = scan_u32(s, A.o_bytes, r.n_reads, tmp, A.total)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_sort_seq, dim3((unsigned)((r.n_reads * 16 + 255) / 256)), dim3(256), 0, s, A);
-        }
+        const int64_t groups = (r.n_reads + kRelayReads - 1) / kRelayReads;
+        hipLaunchKernelGGL(k_sort_relay, dim3((unsigned)((groups * 4 + 255) / 256)), dim3(256), 0, s, A);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     out = r;
@@ -894,9 +776,9 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     out.cig_n = A.o_cig_n;
     out.seq_nib = A.o_seq_nib;
     out.seq = A.o_seq;
-    out.seq_bytes = L.cap;
+    out.seq_bytes = L.room;
     out.qual = A.o_qual;
-    out.qual_bytes = r.qual ? 2 * (int64_t)L.cap : 0;
+    out.qual_bytes = r.qual ? 2 * (int64_t)L.room : 0;
     out.sorted = 1;
     out.seq_layout = BC_SEQ_EVENT;
     out.read_runs = nullptr;
@@ -907,8 +789,8 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     return hipSuccess;
 }
 
-const uint32_t* sort_overflow_word(const bc_reads& r, void* mem) {
-    return (const uint32_t*)((uint8_t*)mem + sort_layout(r).words) + 1;
+const uint32_t* sort_flags_word(const bc_reads& r, const void* mem) {
+    return (const uint32_t*)((const uint8_t*)mem + sort_layout(r).words) + 1;
 }
 
 }  // namespace bc

@@ -60,7 +60,7 @@ struct PileArgs {
     // entropy of the positions >= full_chunks * 8192 (the last partial buffer), at P - that
     int32_t* cov_tail;
     double* ent_tail;
-    // the read-parallel summary (k_sum_reads / k_sum_exact / k_sum_quarters): per 128-position
+    // the read-parallel summary (k_sum_reads / k_sum_exact / k_sum_buffers): per 128-position
     // leaf of the whole buffers, the counted positions of single-read coverage (leaf_cnt) and
     // the slot + 1 of a leaf some position of which two reads cover (leaf_mark, 0 = none); per
     // slot the leaf (dlist) and its exact pairwise sum / coverage (dval / dcov)

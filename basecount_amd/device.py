@@ -82,6 +82,7 @@ def lib() -> C.CDLL:
         "bc_reads_index": ([vp, C.POINTER(BcReads), i64, C.c_int, vp, C.c_size_t], C.c_int),
         "bc_reads_sort_bytes": ([vp, C.POINTER(BcReads), C.POINTER(C.c_size_t)], C.c_int),
         "bc_reads_sort": ([vp, C.POINTER(BcReads), C.POINTER(BcReads), vp, C.c_size_t], C.c_int),
+        "bc_reads_sort_check": ([vp, C.POINTER(BcReads), vp], C.c_int),
         "bc_count": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, vp], C.c_int),
         "bc_range_error": ([vp, C.POINTER(i64)], C.c_int),
         "bc_stats": ([vp, vp, i64, C.c_int, dbl, dbl, vp, vp, vp, vp], C.c_int),
@@ -299,13 +300,23 @@ class Context:
         check(lib().bc_reads_sort_bytes(self.h, C.byref(r), C.byref(n)))
         return int(n.value)
 
-    def sort(self, reads, d_mem, nbytes: int) -> BcReads:
+    def sort(self, reads, d_mem, nbytes: int, check_flags: bool = True) -> BcReads:
         """bc_reads_sort: a coordinate-sorted copy of the batch, built on the device into d_mem
-        (blocking); returns its bc_reads (no index yet)."""
+        (stream-ordered: the call only enqueues); returns its bc_reads (no index yet).  With
+        ``check_flags`` the device's error flags are read at once (sort_check, a sync); without it the
+        caller runs sort_check(reads, d_mem) later, e.g. after the batch's kernels."""
         r = reads.r if isinstance(reads, DeviceReads) else reads
         out = BcReads()
         check(lib().bc_reads_sort(self.h, C.byref(r), C.byref(out), d_mem, int(nbytes)))
+        if check_flags:
+            self.sort_check(r, d_mem)
         return out
+
+    def sort_check(self, reads, d_mem) -> None:
+        """bc_reads_sort_check: waits for the stream, raises BcError (BC_E_ARG) if the sort of
+        ``reads`` into d_mem saw a start outside [0, max_end] or overlapping sequences."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        check(lib().bc_reads_sort_check(self.h, C.byref(r), d_mem))
 
     def pileup(self, reads, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec):
         """Fused kernel 1 + kernel 2 (bc_pileup) for a coordinate-sorted batch: one launch."""

@@ -192,7 +192,10 @@ def rendezvous_init(rank: int, world: int, make_id, init, timeout: float | None 
     def conclude(state: str, why: str, mine: tuple):
         if state == "ok":
             return mine[1]
-        if mine[0] == "ok" and destroy is not None:  # no communicator is left behind
+        # no communicator is left behind -- except on a 'hang' verdict: the process ends right
+        # after (os._exit), and destroying a communicator whose peers are stuck in init could
+        # block and keep it from ever getting there
+        if mine[0] == "ok" and destroy is not None and state != "hang":
             with contextlib.suppress(Exception):
                 destroy(mine[1])
         if state == "hang":
@@ -227,8 +230,13 @@ def rendezvous_init(rank: int, world: int, make_id, init, timeout: float | None 
                 conn.settimeout(init_timeout + timeout)
                 peer = struct.unpack("<I", _recv_exact(conn, 4))[0]
                 conns.append((peer, conn))
-            for _, conn in conns:  # every peer is here: the id goes out to all of them together
-                conn.sendall(struct.pack("<I", len(uid)) + uid)
+            try:  # every peer is here: the id goes out to all of them together
+                for _, conn in conns:
+                    conn.sendall(struct.pack("<I", len(uid)) + uid)
+            except OSError as e:
+                # the peers that already have the id fail at once when their report or the verdict
+                # finds the connection closed (finally, below), instead of waiting out init_timeout
+                raise CommInitError(f"rank 0: sending the communicator id failed ({e})") from e
             if id_err is not None:
                 raise CommInitError(f"rank 0 could not create the communicator id: {id_err}") from id_err
             mine = _run_with_timeout(init, uid, init_timeout)

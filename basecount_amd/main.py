@@ -190,6 +190,15 @@ class _Scratch:
 
     def __init__(self, ctx):
         self.ctx, self.bufs = ctx, {}
+        self.pending_sort = None  # (unsorted reads, sort memory) whose device flags are unread
+
+    def check_sort(self):
+        """The flags of the last device sort (bc_reads_sort_check), read once the reference's
+        kernels are done (the stream is synced by then): the sort itself never waits."""
+        if self.pending_sort is not None:
+            r, mem = self.pending_sort
+            self.pending_sort = None
+            self.ctx.sort_check(r, mem)
 
     def get(self, role: str, nbytes: int):
         b = self.bufs.get(role)
@@ -752,6 +761,7 @@ def _get_basecounts(bam, references, min_base_quality, min_mapping_quality, chun
                                 results[ref] = _finish_reference(ctx, acc.pop(ref), L, ncols, k, nf, nf2, _mode,
                                                                  tiles_of(ref), _tiles is not None, scratch)
                                 finished.add(ref)
+                        scratch.check_sort()
                         if bad >= 0 and ref not in fl.range_:
                             fl.range_[ref] = (base + int(sel.ordinal[b0 + bad]),
                                               _bad_pos(f, int(sel.rec[b0 + bad]), mbq, L))
@@ -913,7 +923,9 @@ def _indexed(ctx, reads: D.BcReads, L: int, scratch: _Scratch) -> D.BcReads:
     against ~0.8 us saved in k_pileup, whose tile groups then search pos[] themselves)."""
     if not reads.sorted and reads.n_reads > 1:
         nb = ctx.sort_bytes(reads)
-        reads = ctx.sort(reads, scratch.get("sorted", nb).ptr, nb)
+        mem = scratch.get("sorted", nb).ptr
+        scratch.pending_sort = (reads, mem)  # checked after the kernels (stream-ordered sort)
+        reads = ctx.sort(reads, mem, nb, check_flags=False)
     return reads
 
 

@@ -182,18 +182,23 @@ int bc_reads_free(bc_ctx* ctx, bc_reads* d_reads);
  * index fields and index_tag of *d_reads.  d_reads->sorted / max_span / max_end must be
  * truthful.  bc_reads_upload builds BC_INDEX_AUTO for ref_len = max_end into its own slab.    */
 /* A coordinate-sorted copy of an unsorted device batch, built on the device (bc_sort.hip):
- * a counting sort of the reads by start position, their per-read arrays written in that order
- * and each read's aligned sequence (and qualities) copied so that consecutive reads have
- * consecutive sequence again.  The copy shares d_reads' CIGAR buffer; everything else lives in
- * d_mem (bc_reads_sort_bytes bytes, 256-byte aligned), which must outlive its use.  *d_sorted
- * is then a sorted batch (sorted = 1, same max_span / max_end, no index: build one with
- * bc_reads_index) that every kernel takes, with the same counts as the input (count.cpp's sums
- * do not depend on the read order).  Needs d_reads->max_end truthful and seq_layout ==
- * BC_SEQ_EVENT; the reads' aligned sequences must not overlap (true of any decoded batch).
- * Blocking: returns after the copy is complete (BC_E_ARG if the sequences did overlap, or if a
- * read starts outside [0, max_end]: device starts are checked, not trusted).                 */
+ * the reads bucketed by start (per-block LDS histograms, one block per bucket ordering it), their
+ * per-read arrays written in start order and each read's aligned sequence (and qualities) copied
+ * so that consecutive reads have consecutive sequence again.  The copy shares d_reads' CIGAR
+ * buffer; everything else lives in d_mem (bc_reads_sort_bytes bytes, 256-byte aligned), which
+ * must outlive its use.  *d_sorted is then a sorted batch (sorted = 1, same max_span / max_end,
+ * no index: build one with bc_reads_index) that every kernel takes, with the same counts as the
+ * input (count.cpp's sums do not depend on the read order).  Needs seq_layout == BC_SEQ_EVENT
+ * and seq_bytes + 5 n_reads + 16 <= 0x55555550 (BC_E_ARG otherwise: split the batch).
+ * Stream-ordered and capturable (round 6): the call only enqueues four kernels; every layout
+ * decision is taken on the device, so there is no host round trip and no fallback path.
+ * Caller errors that only the device can see -- a read starting outside [0, max_end], reads whose
+ * aligned sequences overlap so that the copy would not fit -- leave a flag in d_mem (the sorted
+ * copy stays safe to count: such reads start at 0 / carry no CIGAR): bc_reads_sort_check waits
+ * for the stream and returns BC_E_ARG with the reason if a flag is set, BC_OK otherwise.      */
 int bc_reads_sort_bytes(bc_ctx* ctx, const bc_reads* d_reads, size_t* bytes);
 int bc_reads_sort(bc_ctx* ctx, const bc_reads* d_reads, bc_reads* d_sorted, void* d_mem, size_t bytes);
+int bc_reads_sort_check(bc_ctx* ctx, const bc_reads* d_reads, const void* d_mem);
 
 #define BC_INDEX_RUNS 1
 #define BC_INDEX_TILES 2

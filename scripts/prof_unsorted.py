@@ -20,8 +20,9 @@ counts, cov, pc = ctx.alloc(4 * k * L), ctx.alloc(4 * L), ctx.alloc(8 * k * L)
 ent, sec = ctx.alloc(8 * L), ctx.alloc(8 * L)
 nb = ctx.sort_bytes(reads)
 mem = ctx.alloc(nb)
-for _ in range(20):
-    srt = ctx.sort(reads, mem.ptr, nb)
+for _ in range(20):  # stream-ordered: the sort only enqueues
+    srt = ctx.sort(reads, mem.ptr, nb, check_flags=False)
     ctx.pileup(srt, L, 0, k, nf, nf2, counts.ptr, cov.ptr, pc.ptr, ent.ptr, sec.ptr)
 ctx.sync()
+ctx.sort_check(reads, mem.ptr)
 print("done")

@@ -186,7 +186,8 @@ def test_comm_init_is_agreed_by_every_rank(tmp_path, fail_rank, fail_what):
       ranks whose init succeeded destroyed their communicator (nothing left behind for the
       bench's gloo fallback);
     * an init still blocked at the timeout makes every rank raise CommInitAbandoned instead, and
-      every process exits non-zero within seconds (no fallback next to an abandoned init thread);
+      every process exits non-zero within seconds (no fallback next to an abandoned init thread,
+      and no destroy either: it could block beside the stuck peers);
     * a rank that reaches the rendezvous later than the init timeout does not fail the others:
       rank 0 hands out the id only once every rank is connected."""
     world = 3
@@ -209,8 +210,10 @@ def test_comm_init_is_agreed_by_every_rank(tmp_path, fail_rank, fail_what):
     assert all(r.startswith(want) for _, _, r in res), res
     if fail_what != "id":
         assert all(f"rank {fail_rank}" in r for _, _, r in res), res
-    # every communicator that did come up was destroyed before the error
+    # every communicator that did come up was destroyed before the error -- except on a hang
+    # verdict, where the process ends at once (os._exit) and a destroy next to peers stuck in
+    # init could block it from getting there
     for r, (_, d, _) in enumerate(res):
-        up = fail_what in ("init", "hang") and r != fail_rank
+        up = fail_what == "init" and r != fail_rank
         assert d == (f"[{1000 + r}]" if up else "[]"), (r, d)
 

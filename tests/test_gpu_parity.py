@@ -415,10 +415,11 @@ def test_device_sort_bucket_extremes(ctx, case):
 
 
 @pytest.mark.parametrize("mbq", [0, 30])
-def test_device_sort_exact_path_for_mixed_lengths(ctx, mbq):
-    """A batch of short reads and one 6,000-base read: the fast sort's fixed relay slots (the
-    longest read's bytes each) would not fit the copy's buffer, so bc_reads_sort runs the exact
-    path (counting sort + scanned offsets); same counts, sorted starts."""
+def test_device_sort_shrunk_slots_for_mixed_lengths(ctx, mbq):
+    """A batch of short reads and one 6,000-base read: slots of the longest read's bytes would not
+    fit the copy's buffer, so the device shrinks the slots (half the mean read) and the long read
+    takes its bytes from the bump allocator past them -- decided on the device, no fallback, no
+    host round trip; same counts, sorted starts, no error flag."""
     rng = np.random.default_rng(91)
     L, n = 20_000, 3_000
     pos = [int(x) for x in rng.integers(0, L - 60, n)]
@@ -447,6 +448,93 @@ def test_device_sort_exact_path_for_mixed_lengths(ctx, mbq):
         assert np.array_equal(hist.download(np.int32, 5 * L).reshape(5, L), exp[:, :5].T.astype(np.int32)), shape
         hist.free()
     ctx.set_shape("auto")
+    r.free()
+
+
+def test_device_sort_read_longer_than_16_bits(ctx):
+    """A read of 70,000 query bases (its length does not fit the bucketed record's 16 bits): the
+    record keeps its source index and the copy re-reads its fields and CIGAR; counts exact."""
+    rng = np.random.default_rng(94)
+    L, n = 120_000, 2_000
+    pos = [int(x) for x in rng.integers(0, L - 200, n)]
+    cigs = [[(4, 3), (0, 150)] for _ in range(n)]
+    pos.append(1_000)
+    cigs.append([(0, 69_990), (2, 5), (0, 10)])
+    seqs = [synth.ACGT[rng.integers(0, 4, sum(ln for op, ln in c if op in (0, 1, 4, 7, 8)))] for c in cigs]
+    quals = [rng.integers(0, 45, q.size).astype(np.uint8) for q in seqs]
+    b = build_batch(pos, cigs, seqs, quals, sort=False)
+    exp, (br, _) = O.bcount(L, 0, b)
+    assert br == -1
+    r = D.DeviceReads(ctx, b)
+    nb = ctx.sort_bytes(r)
+    mem = ctx.alloc(nb)
+    s = ctx.sort(r, mem.ptr, nb)
+    hist = ctx.alloc(4 * 5 * L)
+    hist.zero()
+    ctx.count(s, L, 0, 5, hist.ptr)
+    assert ctx.range_error() == -1
+    assert np.array_equal(hist.download(np.int32, 5 * L).reshape(5, L), exp[:, :5].T.astype(np.int32))
+    hist.free()
+    mem.free()
+    r.free()
+
+
+def test_device_sort_flags_are_deferred(ctx):
+    """bc_reads_sort only enqueues: a batch whose max_end is not truthful (a start past it) sorts
+    without an error at the call, and bc_reads_sort_check then reports the bad start (BC_E_ARG);
+    a truthful batch checks clean."""
+    rng = np.random.default_rng(95)
+    L, n = 4_000, 5_000
+    b = random_batch(rng, L, n, sort=False)
+    r = D.DeviceReads(ctx, b)
+    nb = ctx.sort_bytes(r)
+    mem = ctx.alloc(nb)
+    ctx.sort(r, mem.ptr, nb, check_flags=False)
+    ctx.sort_check(r, mem.ptr)  # clean
+    bad = D.BcReads.from_buffer_copy(r.r)
+    bad.max_end = 1_000  # starts beyond it exist
+    nb2 = ctx.sort_bytes(bad)
+    mem2 = ctx.alloc(nb2)
+    s = ctx.sort(bad, mem2.ptr, nb2, check_flags=False)
+    assert s.sorted == 1  # (no error at the call: the device has not run yet)
+    with pytest.raises(D.BcError, match="outside"):
+        ctx.sort_check(bad, mem2.ptr)
+    for x in (mem, mem2):
+        x.free()
+    r.free()
+
+
+def test_device_sort_in_a_graph(ctx):
+    """The sort is capturable: sort + k_rc + kernel 2 of an unsorted C3-shaped batch replayed
+    from one hipGraph twice give the oracle's counts."""
+    rng = np.random.default_rng(96)
+    L, n = 6_000, 120_000
+    b = random_batch(rng, L, n, sort=False)
+    exp, (br, _) = O.bcount(L, 0, b)
+    assert br == -1
+    r = D.DeviceReads(ctx, dict(b, qual=None))
+    nb = ctx.sort_bytes(r)
+    mem = ctx.alloc(nb)
+    k = 5
+    nf, nf2 = norm_factors(k)
+    counts, cov, ent, sec = ctx.alloc(4 * k * L), ctx.alloc(4 * L), ctx.alloc(8 * L), ctx.alloc(8 * L)
+
+    def step():
+        s = ctx.sort(r, mem.ptr, nb, check_flags=False)
+        ctx.pileup(s, L, 0, k, nf, nf2, counts.ptr, cov.ptr, None, ent.ptr, sec.ptr)
+
+    step()  # (scratch allocated outside the capture)
+    ctx.sync()
+    g = ctx.capture(lambda: [step() for _ in range(2)])
+    counts.zero()
+    g.launch()
+    ctx.sync()
+    ctx.sort_check(r, mem.ptr)
+    assert ctx.range_error() == -1
+    assert np.array_equal(counts.download(np.int32, k * L).reshape(k, L), exp[:, :k].T.astype(np.int32))
+    del g
+    for x in (counts, cov, ent, sec, mem):
+        x.free()
     r.free()
 
 
@@ -1007,7 +1095,8 @@ def test_pileup_summary_matches_separate_calls(ctx, L, n, mbq, show_n):
 ])
 def test_summary_only_read_parallel(ctx, L, n, mbq, show_n, layout):
     """The summary-only path of a sparse batch (bc_sum.hip: counted positions per 128-position
-    leaf, exact walks of the leaves two reads share, numpy's tree per quarter) gives exactly the
+    leaf, exact walks of the leaves two reads share, each 8192-position buffer's 64 leaves added
+    in numpy's tree order into whole-buffer partials) gives exactly the
     four numbers numpy computes over the oracle's coverage and entropies (main.py:469-499), with
     mixed CIGARs, quality thresholds, N columns, dense clusters and partial last buffers; and
     again on the same context (its leaf scratch is left zeroed)."""

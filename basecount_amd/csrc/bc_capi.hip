@@ -446,9 +446,20 @@ int bc_reads_index(bc_ctx* c, bc_reads* r, int64_t L, int what, void* d_mem, siz
     return BC_OK;
 }
 
+// The sort leaves the sequence in place (sorts the fields + run records only) when the sorted
+// batch will take the read-chunked k_rc, which gathers a chunk's scattered reads into LDS itself;
+// batches with qualities (a quality threshold: k_rc's variants that stage through registers) and
+// the tiled kernels' shallower batches get the sequence copied into start order.
+static bool sort_fields_only(const bc_ctx* c, const bc_reads& r) {
+    if (r.qual) return false;
+    bc_reads v = r;
+    v.sorted = 1;
+    return bc::use_rc(v, r.max_end, c->shape);
+}
+
 int bc_reads_sort_bytes(bc_ctx* c, const bc_reads* r, size_t* bytes) {
     if (!c || !r || !bytes) return fail(BC_E_ARG, "NULL argument");
-    *bytes = bc::sort_bytes(*r);
+    *bytes = bc::sort_bytes(*r, sort_fields_only(c, *r));
     return BC_OK;
 }
 
@@ -463,7 +474,8 @@ int bc_reads_sort(bc_ctx* c, const bc_reads* r, bc_reads* out, void* d_mem, size
     }
     if (r->seq_layout != BC_SEQ_EVENT) return fail(BC_E_ARG, "bc_reads_sort needs seq_layout == BC_SEQ_EVENT");
     if (!r->pos || !r->cig_beg || !r->cig_n || !r->seq_nib || !r->seq) return fail(BC_E_ARG, "bc_reads_sort: missing array");
-    const size_t need = bc::sort_bytes(*r);
+    const bool fields = sort_fields_only(c, *r);
+    const size_t need = bc::sort_bytes(*r, fields);
     if (!d_mem || bytes < need) return fail(BC_E_ARG, "bc_reads_sort: d_mem smaller than bc_reads_sort_bytes");
     if ((uintptr_t)d_mem & 255u) return fail(BC_E_ARG, "bc_reads_sort: d_mem must be 256-byte aligned");
     if (!bc::sort_fits(*r))
@@ -473,7 +485,7 @@ int bc_reads_sort(bc_ctx* c, const bc_reads* r, bc_reads* out, void* d_mem, size
     bc_reads tmp;
     {
         Timed tm(c, BC_K_SORT);
-        HIP_TRY(bc::launch_sort(c->stream, *r, tmp, d_mem));
+        HIP_TRY(bc::launch_sort(c->stream, *r, tmp, d_mem, fields));
     }
     *out = tmp;
     return BC_OK;

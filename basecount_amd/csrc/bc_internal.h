@@ -114,10 +114,13 @@ inline bool pileup_is_solo(const bc_reads& r, int64_t L, int shape, int tile_wav
 }
 
 // ---- the coordinate-sorted copy of an unsorted batch (bc_sort.hip) ----
-size_t sort_bytes(const bc_reads& r);
-// enqueues the sort into mem (sort_bytes(r) bytes; stream-ordered, no host round trip) and fills
-// `out` (sorted, no index); needs sort_fits(r)
-hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem);
+// fields: sort only the per-read fields (+ run records) and leave the sequence where it is (k_rc
+// stages a chunk's scattered reads by LDS-DMA gathers); else copy the sequence (and qualities)
+// into start order as well
+size_t sort_bytes(const bc_reads& r, bool fields);
+// enqueues the sort into mem (sort_bytes(r, fields) bytes; stream-ordered, no host round trip)
+// and fills `out` (sorted; no index, or with fields the run records); needs sort_fits(r)
+hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem, bool fields);
 bool sort_fits(const bc_reads& r);
 // device word of caller errors (read after a sync): bit 0 the reads' sequences overlap (the copy
 // did not fit), bit 1 a start outside [0, max_end]

@@ -69,6 +69,14 @@ constexpr bool kEarlyWait = BC_RC_EARLY_WAIT != 0;
 constexpr bool kGather = BC_RC_GATHER != 0;
 constexpr int kRcSlot = 76;  // stage bytes per read in gather staging (152 nibbles: 150-bp reads at either parity)
 static_assert(kRcSlot % 4 == 0 && kRcSlot * kRcChunk <= 78 * kRcChunk, "gather slots fit the stage");
+// Transposed gather staging (image chunks of a batch sorted on the device without moving its
+// sequence, bc_sort.hip's fields-only sort): each read's bytes from the 4-byte word holding its
+// first base, kGWords words, by LDS-DMA one word per lane (instruction e of a wave: word e of its
+// 64 reads, 256 contiguous LDS bytes), so the stage is [wave][word][lane]: a lane's words are 64
+// words apart and a wave reading one word of each of its reads hits 64 different banks, whatever
+// the reads' offsets (the linear stage's reads at unrelated offsets collide).
+constexpr int kGWords = 20;  // 80 bytes: a read of <= 77 bytes at any byte offset in its first word
+constexpr int kGStage = 4 * kGWords * kRcChunk;
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
 constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
 
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     __shared__ uint4 rec[kRecU4 > kImgU4 + kImgPadU4 ? kRecU4 : kImgU4 + kImgPadU4];
     uint32_t* img = (uint32_t*)rec;
     __shared__ int32_t rpos[kRcReads];  // the chunk's read positions (window tables)
-    __shared__ __attribute__((aligned(16))) uint8_t stage_raw[kStage + 8 * kPadW];  // + pads
+    __shared__ __attribute__((aligned(16))) uint8_t stage_raw[(kStage > kGStage ? kStage : kGStage) + 8 * kPadW];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
     __shared__ __attribute__((aligned(16))) uint32_t red[kRcWaves][8];
     __shared__ uint32_t wlo[kRcWin], whi[kRcWin], wpre[kRcWin + 1];
@@ -533,20 +541,28 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // Only when every simple read fits its slot (a chunk of long reads would walk
         // most of them as complex reads, one per wave with global atomics, where the run-table walk
         // from HBM is the better fallback).
-        const bool gather = kGather && !QUAL && !staged && !sums && v[7] <= (uint32_t)kRcSlot &&
-                            !(BC_ABL(A) & 512);  // (uniform)
-        const bool big = gather && simple && ((((msn & 1u) + T.qlen + 1u) >> 1) > (uint32_t)kRcSlot);
-        const bool cxa = cx || big, simplea = simple && !big;
-        const bool inlds = staged || gather;  // (uniform) the walks read the stage
-        // the read's first base as a nibble index of the stage (or of the batch's buffer)
-        const uint32_t rel = gather ? (uint32_t)(2 * kRcSlot * tid) + (msn & 1u) : msn - (staged ? 2u * seg_lo : 0u);
-        if (cxa) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         // event-image path: a staged chunk of reads with <= 2 runs whose windows fit the image.
         // Each read's events are extracted ONCE per window (lane = read, its windows in a row)
         // instead of once per (window, run) item from the run table.
         const IT WBc = P0 & ~(IT)7;
         const int NWc = (int)(P1 > WBc ? (P1 - WBc + 7) / 8 : 0);
-        const bool img_path = inlds && maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);
+        const bool img_shape = maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);  // (uniform)
+        // an image chunk takes the transposed gather, a run-table chunk the linear slots
+        const bool gather_t = kGather && !QUAL && !staged && !sums && img_shape && v[7] <= 4u * kGWords - 3u &&
+                              !(BC_ABL(A) & 512);  // (uniform)
+        const bool gather = kGather && !QUAL && !staged && !sums && !gather_t && v[7] <= (uint32_t)kRcSlot &&
+                            !(BC_ABL(A) & 512);  // (uniform)
+        const uint32_t rbytes = ((msn & 1u) + T.qlen + 1u) >> 1;  // the read's sequence bytes
+        const bool big = simple && ((gather && rbytes > (uint32_t)kRcSlot) ||
+                                    (gather_t && ((msn >> 1) & 3u) + rbytes > 4u * kGWords));
+        const bool cxa = cx || big, simplea = simple && !big;
+        const bool inlds = staged || gather || gather_t;  // (uniform) the walks read the stage
+        // the read's first base as a nibble index of the stage (or of the batch's buffer); in the
+        // transposed stage, of the read's own column
+        const uint32_t rel = gather_t ? (msn & 7u)
+                             : gather ? (uint32_t)(2 * kRcSlot * tid) + (msn & 1u) : msn - (staged ? 2u * seg_lo : 0u);
+        if (cxa) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
+        const bool img_path = inlds && img_shape;
         const int gpad = NWc;  // (uniform) the image's group padding (see rec)
         uint32_t* const mycol = img + tid * kImgRows + (tid >> 5) * gpad;  // this read's image column
         if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
@@ -581,6 +597,18 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 }
                 *(uint4*)(stage + off) = q4;
             }
+        }
+        if (gather_t && simplea) {
+            // the read's words (from the one holding its first base) into its column of the
+            // wave's [word][lane] block: word e of every read of the wave is one LDS-DMA
+            // instruction (a lane's address; the destination 64 consecutive words)
+            const uint8_t* src = A.seq + ((msn >> 1) & ~3u);
+            const uint32_t nw = (((msn >> 1) & 3u) + rbytes + 3u) >> 2;
+            uint8_t* dst = stage + wave * (4 * 64 * kGWords);
+#pragma unroll
+            for (int e = 0; e < kGWords; ++e)
+                if ((uint32_t)e < nw)
+                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 4 * e), (lds_void_t*)(dst + 256 * e), 4, 0, 0);
         }
         if (gather && simplea) {
             // the read's bytes from its first base on, 4-byte words funnel-shifted from the aligned
@@ -636,16 +664,25 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             // run k's stage word of row r is f_k + r (+1 for the funnel's upper word): within
             // [-kPadW + 1, kStage / 4 + kPadW - 1] for every simple read (f_k >= -1 - 22, the
             // read's sequence lies in the stage), so the stage's pads absorb it unclamped
-            const uint32_t* w0 = (const uint32_t*)stage + (wb0 - i0);
-            const uint32_t* w1 = (const uint32_t*)stage + (wb1 - i0);
+            // run k's stage word for row r: w_k[r * S] (S = 1: the linear stage; S = 64: the
+            // transposed gather stage, the lane's column of its wave's [word][lane] block; rows
+            // outside the read read words that the masks discard)
+            auto colp = [&](int wb, auto st_c) -> const uint32_t* {
+                constexpr int S = decltype(st_c)::value;
+                return S == 1 ? (const uint32_t*)stage + (wb - i0)
+                              : (const uint32_t*)stage + wave * (64 * kGWords) + lane + 64 * (wb - i0);
+            };
             // Row r's 8 event classes, all rows unrolled without branches so the LDS reads of
             // later rows issue ahead.  ge(X): the row's stream bits at or above X, i.e. bits
             // >= d = clamp(X - 32r, 0, 32).  The clamp is one med3 of X against [32r, 32r + 32]
             // (constants the compiler keeps in registers), and 0xFFFFFFFF << (m mod 64) as 64
             // bits holds the mask in its low word (even r: m mod 64 = d) or its high word (odd r:
             // 32 + d, or 0 when d = 32).
-            auto expand = [&](auto two_c, auto edge_c) {
+            auto expand = [&](auto two_c, auto edge_c, auto st_c) {
                 constexpr bool TWO = decltype(two_c)::value, EDGE = decltype(edge_c)::value;
+                constexpr int S = decltype(st_c)::value;
+                const uint32_t* w0 = colp(wb0, st_c);
+                const uint32_t* w1 = colp(wb1, st_c);
                 const int yz = Z, yb = B0e, ya = A1, ys = SP;
                 uint32_t p0 = w0[0], p1 = TWO ? w1[0] : 0u;
 #pragma unroll
@@ -658,12 +695,12 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                         return (row & 1) ? (uint32_t)(v >> 32) : (uint32_t)v;
                     };
                     const uint32_t gz = ge(yz), gb = ge(yb);
-                    const uint32_t n0 = w0[row + 1];
+                    const uint32_t n0 = w0[(row + 1) * S];
                     uint32_t x = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n0, p0, sh0), gz, gb, 0x40);
                     p0 = n0;
                     if (TWO) {
                         const uint32_t ga = ge(ya), gs = ge(ys);
-                        const uint32_t n1 = w1[row + 1];
+                        const uint32_t n1 = w1[(row + 1) * S];
                         const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n1, p1, sh1), ga, gs, 0x40);
                         // (independent terms: a select chain measured slower, 57 vs 54 us)
                         // s0 & s1 & ~s2 (0x40); then s0 | s1 | s2 (0xFE) in one op
@@ -693,13 +730,16 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 const int lo = (a + 31) >> 5, hi = b >> 5;
                 return hi > lo ? lo32_bit(hi) - lo32_bit(lo) : 0u;
             };
-            auto interior = [&]() {
+            auto interior = [&](auto st_c) {
+                constexpr int S = decltype(st_c)::value;
+                const uint32_t* w0 = colp(wb0, st_c);
+                const uint32_t* w1 = colp(wb1, st_c);
                 const uint32_t o0 = rowmask(Z, B0e), o1 = rowmask(A1, SP);
                 uint32_t p0 = w0[0], p1 = w1[0];
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) {
                     if (row >= kImgRows - 4 && row >= NWc) continue;  // (uniform) past the chunk
-                    const uint32_t n0 = w0[row + 1], n1 = w1[row + 1];
+                    const uint32_t n0 = w0[(row + 1) * S], n1 = w1[(row + 1) * S];
                     const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)o0, row, 1);
                     const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)o1, row, 1);
                     const uint32_t x1 = __builtin_amdgcn_alignbit(n1, p1, sh1) & m1;
@@ -723,8 +763,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     for (int k = 0; k < 4; ++k) {
                         const int rb = bs[k] >> 5;
                         rbs[k] = rb < kImgRows - 1 ? rb : kImgRows - 1;
-                        q0[k] = make_uint2(w0[rbs[k]], w0[rbs[k] + 1]);
-                        q1[k] = make_uint2(w1[rbs[k]], w1[rbs[k] + 1]);
+                        q0[k] = make_uint2(w0[rbs[k] * S], w0[(rbs[k] + 1) * S]);
+                        q1[k] = make_uint2(w1[rbs[k] * S], w1[(rbs[k] + 1) * S]);
                     }
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
@@ -745,9 +785,12 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) mycol[row] = 0u;
             } else if (8 * (IT)(G0 + kImgRows) > L) {  // (uniform) rows may reach past L
-                expand(std::true_type{}, std::true_type{});
+                if (gather_t) expand(std::true_type{}, std::true_type{}, std::integral_constant<int, 64>{});
+                else expand(std::true_type{}, std::true_type{}, std::integral_constant<int, 1>{});
+            } else if (gather_t) {  // (uniform)
+                interior(std::integral_constant<int, 64>{});
             } else {
-                interior();
+                interior(std::integral_constant<int, 1>{});
             }
         }
         pf_ok = false;

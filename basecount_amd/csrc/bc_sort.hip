@@ -27,7 +27,7 @@
 namespace bc {
 namespace {
 
-#include "bc_runs.h"
+#include "bc_walk.h"
 
 constexpr int kScanTile = 1024;  // elements per scan block (256 threads x 4)
 
@@ -151,6 +151,10 @@ struct SortArgs {
     uint32_t* bstat;    // [nblk][2]: block b's largest query length, its flags
     uint4* brec;        // [n] {pos, cig_beg, seq_nib, cig_n | qlen << 16} in bucket order
     uint4* srec;        // [n] the same in start order
+    // fields-only sorts (no sequence copy): each read's run record (bc_runs.h pack_runs) in bucket
+    // order, and the sorted batch's run records
+    uint4* brun;
+    uint4* o_runs;
     int64_t chunk;
     int nblk, nbkt, wbits;
 };
@@ -433,6 +437,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(SortArgs A) {
     for (int h = threadIdx.x; h < H; h += kBktThreads) A.mat[(int64_t)blockIdx.x * H + h] = hist[h];
 }
 
+template <bool FIELDS>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     __shared__ uint32_t next[kBktMax], pre[kBktMax];
     __shared__ uint32_t ws[kBktThreads / 64];
@@ -508,6 +513,24 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
         for (int u = 0; u < B; ++u)
 #pragma unroll
             for (int k = 0; k < 8; ++k) w[u][k] = (uint32_t)k < cn[u] ? A.cigar[cb[u] + k] : 0u;
+        if (FIELDS) {  // no copy: the record and the read's run record (k_rc then decodes nothing)
+            int cm[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)  // ops decoded: the wave's longest CIGAR (up to kPre), outside the tail's branch
+                cm[u] = (int)(uint32_t)__builtin_amdgcn_readfirstlane(
+                    (int)wave_reduce<true>(i0 + (int64_t)u * kBktThreads < end ? (cn[u] < (uint32_t)kPre ? cn[u] : (uint32_t)kPre) : 0u));
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const int64_t i = i0 + (int64_t)u * kBktThreads;
+                if (i >= end) break;
+                uint32_t rr[4];
+                pack_runs(decode_runs<2>(w[u], cn[u], cm[u]), rr);
+                const uint32_t j = atomicAdd(&next[p[u] >> A.wbits], 1u);
+                A.brec[j] = make_uint4(p[u], cb[u], sn[u], cn[u]);
+                A.brun[j] = make_uint4(rr[0], rr[1], rr[2], rr[3]);
+            }
+            continue;
+        }
 #pragma unroll
         for (int u = 0; u < B; ++u) {
             const int64_t i = i0 + (int64_t)u * kBktThreads;
@@ -544,6 +567,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     }
 }
 
+template <bool FIELDS>
 __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     __shared__ uint32_t cnt[kBktLowMax];
     __shared__ uint32_t ws[kRankThreads / 64];
@@ -554,11 +578,26 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     const int W = 1 << A.wbits;
     const uint32_t lo_mask = (uint32_t)W - 1u;
     uint4 rec[kRankRegs];  // the bucket's first kRankRegs * kRankThreads records
+    uint4 run[FIELDS ? kRankRegs : 1];
 #pragma unroll
     for (int k = 0; k < kRankRegs; ++k) {
         const uint32_t r = bs + t + k * kRankThreads;
         rec[k] = r < be ? A.brec[r] : make_uint4(0u, 0u, 0u, 0u);
+        if (FIELDS) run[k] = r < be ? A.brun[r] : make_uint4(0u, 0u, 0u, 0u);
     }
+    // the record of sorted slot j: its start-ordered copy (srec), or with FIELDS the sorted
+    // batch's own arrays (the sequence stays where it is: seq_nib is the source's)
+    auto put = [&](uint32_t j, const uint4& x, const uint4& y) {
+        if (FIELDS) {
+            A.o_pos[j] = (int32_t)x.x;
+            A.o_cig_beg[j] = x.y;
+            A.o_seq_nib[j] = x.z;
+            A.o_cig_n[j] = x.w;
+            A.o_runs[j] = y;
+        } else {
+            A.srec[j] = x;
+        }
+    };
     if (h == 0) {  // the batch's largest query length and flags; the copy's zero padding
         uint32_t qm = 0, fl = 0;
         for (int b = t; b < A.nblk; b += kRankThreads) {
@@ -580,8 +619,10 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
             *A.overflow = rf;  // (bit 1: a bad start; the copy may add bit 0)
             *A.bump = 0u;
         }
-        const size_t pad0 = A.room, pad1 = ((size_t)A.room + 15) / 16 * 16 + 16;  // seq_event_bytes(room): zero
-        for (size_t at = pad0 + t; at < pad1; at += kRankThreads) A.o_seq[at] = 0;
+        if (!FIELDS) {
+            const size_t pad0 = A.room, pad1 = ((size_t)A.room + 15) / 16 * 16 + 16;  // seq_event_bytes(room): zero
+            for (size_t at = pad0 + t; at < pad1; at += kRankThreads) A.o_seq[at] = 0;
+        }
     }
     for (int k = t; k < W; k += kRankThreads) cnt[k] = 0u;
     __syncthreads();
@@ -594,10 +635,10 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     lds_scan_excl<kRankThreads, kBktLowMax / kRankThreads>(cnt, W, ws);
 #pragma unroll
     for (int k = 0; k < kRankRegs; ++k)
-        if (bs + t + k * kRankThreads < be) A.srec[bs + atomicAdd(&cnt[rec[k].x & lo_mask], 1u)] = rec[k];
+        if (bs + t + k * kRankThreads < be) put(bs + atomicAdd(&cnt[rec[k].x & lo_mask], 1u), rec[k], run[FIELDS ? k : 0]);
     for (uint32_t r = more + t; r < be; r += kRankThreads) {
         const uint4 x = A.brec[r];
-        A.srec[bs + atomicAdd(&cnt[x.x & lo_mask], 1u)] = x;
+        put(bs + atomicAdd(&cnt[x.x & lo_mask], 1u), x, FIELDS ? A.brun[r] : x);
     }
 }
 
@@ -664,16 +705,18 @@ BktPlan bkt_plan(const bc_reads& r) {
 }
 
 struct SortLayout {
-    size_t bins, rec, o_pos, o_cb, o_cn, o_sn, tmp, words, o_seq, o_qual, mat, bstat, bbase, total;
+    size_t bins, rec, o_pos, o_cb, o_cn, o_sn, o_runs, tmp, words, o_seq, o_qual, mat, bstat, bbase, total;
     int64_t nbins;
     uint32_t cap, room;
     BktPlan bkt;
 };
 
-SortLayout sort_layout(const bc_reads& r) {
+// fields: the bucketed sort without the sequence copy (sort_fields_only)
+SortLayout sort_layout(const bc_reads& r, bool fields) {
     SortLayout L{};
     const int64_t n = r.n_reads;
     L.bkt = bkt_plan(r);
+    fields = fields && L.bkt.ok;
     const int64_t mat_words = L.bkt.ok ? (int64_t)L.bkt.nbkt * L.bkt.nblk : 0;
     L.nbins = r.max_end + 2;  // every start <= max_end
     // every read takes its aligned bases' bytes rounded up to 4 (+ 1 for an odd start); the copy's
@@ -686,16 +729,17 @@ SortLayout sort_layout(const bc_reads& r) {
         off += (bytes + 255) / 256 * 256;
         return at;
     };
+    L.words = take(16);  // bump, flags, qmax: first, at the same offset in every layout
     L.bins = L.bkt.ok ? 0 : take(4 * (size_t)L.nbins);
     L.rec = take(32 * (size_t)n);
     L.o_pos = take(4 * (size_t)n);
     L.o_cb = take(4 * (size_t)n);
     L.o_cn = take(4 * (size_t)n);
     L.o_sn = take(4 * (size_t)n);
+    L.o_runs = fields ? take(16 * (size_t)n) : 0;
     L.tmp = L.bkt.ok ? 0 : take(4 * scan_tmp_words(L.nbins));
-    L.words = take(16);  // bump, flags, qmax
-    L.o_seq = take(seq_event_bytes(L.room));
-    L.o_qual = r.qual ? take(2 * (size_t)L.room + 32) : 0;
+    L.o_seq = fields ? 0 : take(seq_event_bytes(L.room));
+    L.o_qual = (r.qual && !fields) ? take(2 * (size_t)L.room + 32) : 0;
     L.mat = take(4 * (size_t)mat_words);
     L.bstat = take(8 * (size_t)(L.bkt.ok ? L.bkt.nblk : 0));
     L.bbase = take(4 * (size_t)(L.bkt.ok ? L.bkt.nbkt + 1 : 0));
@@ -705,15 +749,16 @@ SortLayout sort_layout(const bc_reads& r) {
 
 }  // namespace
 
-size_t sort_bytes(const bc_reads& r) {
+size_t sort_bytes(const bc_reads& r, bool fields) {
     if (r.n_reads <= 0) return 0;
-    return sort_layout(r).total;
+    return sort_layout(r, fields).total;
 }
 
 bool sort_fits(const bc_reads& r) { return r.seq_bytes + 5 * r.n_reads + 16 <= kSortCapMax; }
 
-hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem) {
-    const SortLayout L = sort_layout(r);
+hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* mem, bool fields) {
+    const SortLayout L = sort_layout(r, fields);
+    fields = fields && L.bkt.ok;
     uint8_t* b = (uint8_t*)mem;
     SortArgs A{};
     A.pos = r.pos;
@@ -751,11 +796,18 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
         A.nbkt = L.bkt.nbkt;
         A.wbits = L.bkt.wbits;
         hipLaunchKernelGGL(k_bkt_count, dim3((unsigned)A.nblk), dim3(kBktThreads), 0, s, A);
-        hipLaunchKernelGGL(k_bkt_scatter, dim3((unsigned)A.nblk), dim3(kBktThreads), 0, s, A);
-        hipLaunchKernelGGL(k_bkt_rank, dim3((unsigned)A.nbkt), dim3(kRankThreads), 0, s, A);
-        // one slot per lane group (a wave: 16 slots): 93 us against 95 / 98 / 101 at 2 / 4 / 8
-        const int64_t waves = (r.n_reads + 15) / 16;
-        hipLaunchKernelGGL(k_bkt_copy<1>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, A);
+        if (fields) {  // the sorted fields and run records; the sequence stays where it is
+            A.brun = A.rec + r.n_reads;
+            A.o_runs = (uint4*)(b + L.o_runs);
+            hipLaunchKernelGGL(k_bkt_scatter<true>, dim3((unsigned)A.nblk), dim3(kBktThreads), 0, s, A);
+            hipLaunchKernelGGL(k_bkt_rank<true>, dim3((unsigned)A.nbkt), dim3(kRankThreads), 0, s, A);
+        } else {
+            hipLaunchKernelGGL(k_bkt_scatter<false>, dim3((unsigned)A.nblk), dim3(kBktThreads), 0, s, A);
+            hipLaunchKernelGGL(k_bkt_rank<false>, dim3((unsigned)A.nbkt), dim3(kRankThreads), 0, s, A);
+            // one slot per lane group (a wave: 16 slots): 93 us against 95 / 98 / 101 at 2 / 4 / 8
+            const int64_t waves = (r.n_reads + 15) / 16;
+            hipLaunchKernelGGL(k_bkt_copy<1>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, A);
+        }
     } else {  // more than 2^24 starts: the counting sort with one global atomic per read
         A.bins = (uint32_t*)(b + L.bins);
         uint32_t* tmp = (uint32_t*)(b + L.tmp);
@@ -771,6 +823,20 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     out = r;
+    if (fields) {  // the source's sequence, CIGARs and (no) qualities; run records, no summaries
+        out.pos = A.o_pos;
+        out.cig_beg = A.o_cig_beg;
+        out.cig_n = A.o_cig_n;
+        out.seq_nib = A.o_seq_nib;
+        out.sorted = 1;
+        out.seq_layout = BC_SEQ_EVENT;
+        out.read_runs = (const uint32_t*)A.o_runs;
+        out.run_chunks = 0;
+        out.tile_reads = nullptr;
+        out.n_tiles = 0;
+        out.index_tag = index_tag(out);
+        return hipSuccess;
+    }
     out.pos = A.o_pos;
     out.cig_beg = A.o_cig_beg;
     out.cig_n = A.o_cig_n;
@@ -790,7 +856,7 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
 }
 
 const uint32_t* sort_flags_word(const bc_reads& r, const void* mem) {
-    return (const uint32_t*)((const uint8_t*)mem + sort_layout(r).words) + 1;
+    return (const uint32_t*)((const uint8_t*)mem + sort_layout(r, false).words) + 1;  // (offset 0 in every layout)
 }
 
 }  // namespace bc

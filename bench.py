@@ -191,14 +191,13 @@ def cpu_baseline(rs, b, L: int, budget_s: float = 10.0, mbq: int = 0, what: str 
         reads, quals, starts, ctuples = args if args is not None else pysam_args(rs, 0)
         dt, done = _loop(lambda: O.get_stats_py(ref(L, mbq, reads, quals, starts, ctuples), "ref"), budget_s)
         del reads, quals, starts, ctuples
-        kind, desc = "reference", ("reference count.cpp (pybind11 bcount, list arguments) + "
-                                   "get_stats main.py:14-79 (Python)")
+        kind, desc = "reference", "count.cpp bcount (pybind11) + get_stats main.py:14-79"
     else:
         dt, done = _loop(lambda: O.stats(O.bcount(L, mbq, b)[0], False), budget_s)
-        kind, desc = "port", "oracle C restatement of bcount + get_stats"
+        kind, desc = "port", "oracle C bcount + get_stats"
     return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind,
-            "sample": f"{desc}; full {what} workload ({n} reads, {L} positions, min_base_quality {mbq}) x "
-                      f"{done} runs, {dt * 1e3:.1f} ms per run, BAM decode excluded"}
+            "sample": f"{desc}; full {what} ({n} reads, {L} positions, mbq {mbq}) x {done}, "
+                      f"{dt * 1e3:.1f} ms each, no BAM decode"}
 
 
 def cpu_baseline_c4(b, L: int, args, budget_s: float = 5.0) -> dict:
@@ -222,17 +221,16 @@ def cpu_baseline_c4(b, L: int, args, budget_s: float = 5.0) -> dict:
         def run():
             rows = O.get_stats_py(ref(L, 0, *args), "ref")
             O.summary_amplicons_py(rows, tiles)
-        kind, desc = "reference", "reference count.cpp (pybind11 bcount) + get_stats + main.py:469-551 summary and amplicon loops"
+        kind, desc = "reference", "count.cpp bcount + get_stats + main.py:469-551 loops"
     else:
         def run():
             rows = O.get_stats_py(O.bcount(L, 0, b)[0].tolist(), "ref")
             O.summary_amplicons_py(rows, tiles)
-        kind, desc = "port", "oracle C restatement of bcount + get_stats + main.py:469-551 summary and amplicon loops"
+        kind, desc = "port", "oracle C bcount + get_stats + main.py:469-551 loops"
     dt, done = _loop(run, budget_s)
     return {"value": L / dt, "unit": "positions/s", "cores": 1, "kind": kind,
-            "sample": f"{desc} (Python, restated in oracle.summary_amplicons_py); full C4 workload ({n} reads, "
-                      f"{L} positions, {len(tiles)} amplicon windows) x {done} runs, {dt * 1e3:.1f} ms per run, "
-                      "BAM decode excluded"}
+            "sample": f"{desc} (oracle.summary_amplicons_py); full C4 ({n} reads, {L} positions, "
+                      f"{len(tiles)} windows) x {done}, {dt * 1e3:.1f} ms each, no BAM decode"}
 
 
 def cpu_baseline_all_cores(b, L: int, budget_s: float = 5.0) -> dict:
@@ -244,9 +242,7 @@ def cpu_baseline_all_cores(b, L: int, budget_s: float = 5.0) -> dict:
     T = cpu_threads()
     dt, done = _loop(lambda: O.stats(O.bcount(L, 0, b, nthreads=T)[0], False, nthreads=T), budget_s)
     return {"value": L / dt, "unit": "positions/s", "cores": T, "kind": "port",
-            "sample": f"oracle C restatement of bcount + get_stats on {T} threads; full C2 workload "
-                      f"({int(b['pos'].size)} reads, {L} positions) x {done} runs, {dt * 1e3:.2f} ms "
-                      f"per run, BAM decode excluded"}
+            "sample": f"oracle C bcount + get_stats, {T} threads; full C2 x {done}, {dt * 1e3:.2f} ms each"}
 
 
 def e2e(cfg: str, summarise: bool = False) -> dict:
@@ -373,11 +369,15 @@ class Workload:
                 r = D.DeviceReads(ctx, dict(b, seq_event=ev))
                 self.upload_s += time.perf_counter() - t_up
                 assert r.r.sorted == 1
-                if not tile_index:  # A/B: the tiled kernel searches pos[] (the index stays allocated)
+                # as the CLI counts a batch (main._indexed builds no index): the tiled kernel searches
+                # pos[], the read-chunked one decodes the CIGARs (single pass); the upload's index
+                # (built outside the timed region) only for the --tile-index / --read-runs A/B
+                if not tile_index:
                     r.r.tile_reads = None
                     r.r.n_tiles = 0
-                if not read_runs:  # the read-chunked kernel decodes the CIGARs itself (single pass)
+                if not read_runs:
                     r.r.read_runs = None
+                    r.r.run_chunks = 0
                 reads.append(r)
             self.h2d_bytes += self.copies * (16 * int(b["pos"].size) + 4 * int(b["cigar"].size) + ev.size)
             k = self.k
@@ -572,6 +572,11 @@ class Workload:
             x.free()
         self.d_tiles = None
         self.work = []
+
+
+def strip_index(r) -> None:
+    """A bc_reads without its upload-built device index (what main._indexed hands the kernels)."""
+    r.read_runs, r.run_chunks, r.tile_reads, r.n_tiles, r.index_tag = None, 0, None, 0, 0
 
 
 def compact(x, digits: int = 4):
@@ -1067,6 +1072,8 @@ def run_unsorted(ctx, args, reps: int = 20) -> dict:
     b3 = synth.batch_arrays(synth.make_config("c3"), 0, 0)
     ev3 = seq_to_event(b3["seq"])
     srt_in = [D.DeviceReads(ctx, dict(b3, qual=None, seq_event=ev3)) for _ in range(copies)]
+    for r in srt_in:
+        strip_index(r.r)  # as the CLI counts it: no device index (main._indexed)
     turn3 = [0]
 
     def sorted_step():
@@ -1368,7 +1375,10 @@ def main():
         line["gather_ms"] = gather_ms
         # the extras in the order the judge reads them (a long line's head can be cut): the deep
         # configs first, the end-to-end CLI timings last
-        line["extra"] = {k: extra[k] for k in ("c3", "c3_unsorted", "c4", "c3_q20", "c5", "c2", "c3_split") if k in extra}
+        drop = ("reads_per_rank", "positions_per_rank", "contigs_per_rank", "streams", "steps", "warmup", "unit",
+                "upload_ms", "launch_trial_us")
+        line["extra"] = {k: {f: v for f, v in extra[k].items() if f not in drop}
+                         for k in ("c3", "c3_unsorted", "c4", "c3_q20", "c5", "c2", "c3_split") if k in extra}
         line["e2e"] = e2e_res
         for cfg in ("c3", "c5"):
             if cfg in line["extra"] and "e2e" in line["extra"][cfg]:

@@ -315,9 +315,13 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // the image's 32-read groups are R words apart beyond their 736 (R = the chunk's rows, <= 23),
     // so the sum's lanes (row t mod R of group t / R) read 32 consecutive banks
     constexpr int kImgPadU4 = (7 * kImgRows + 3) / 4;
-    __shared__ uint4 rec[kRecU4 > kImgU4 + kImgPadU4 ? kRecU4 : kImgU4 + kImgPadU4];
+    constexpr int kRecAll = kRecU4 + kRcReads / 4;  // records + the read positions (run-table chunks)
+    __shared__ uint4 rec[kRecAll > kImgU4 + kImgPadU4 ? kRecAll : kImgU4 + kImgPadU4];
     uint32_t* img = (uint32_t*)rec;
-    __shared__ int32_t rpos[kRcReads];  // the chunk's read positions (window tables)
+    // the chunk's read positions (window tables of the run-table walk), past its records: the
+    // image path, which overwrites both, uses neither (1 KiB of LDS kept for the gather stage:
+    // a 512-byte larger block no longer fits three times into a CU, k_rc 46 -> 71 us at C3)
+    int32_t* const rpos = (int32_t*)(rec + kRecU4);
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[(kStage > kGStage ? kStage : kGStage) + 8 * kPadW];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
     __shared__ __attribute__((aligned(16))) uint32_t red[kRcWaves][8];

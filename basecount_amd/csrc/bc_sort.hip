@@ -567,9 +567,11 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     }
 }
 
+constexpr int kPermSlots = 1024;  // fields-only rank: sorted slots per LDS pass (32 KiB)
 template <bool FIELDS>
 __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     __shared__ uint32_t cnt[kBktLowMax];
+    __shared__ uint4 perm_rec[FIELDS ? kPermSlots : 1], perm_run[FIELDS ? kPermSlots : 1];
     __shared__ uint32_t ws[kRankThreads / 64];
     __shared__ uint32_t rq, rf;
     const int h = blockIdx.x, t = threadIdx.x;
@@ -633,6 +635,28 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     for (uint32_t r = more + t; r < be; r += kRankThreads) atomicAdd(&cnt[A.brec[r].x & lo_mask], 1u);
     __syncthreads();
     lds_scan_excl<kRankThreads, kBktLowMax / kRankThreads>(cnt, W, ws);
+    if (FIELDS && be - bs <= (uint32_t)(kRankRegs * kRankThreads)) {  // (uniform) the bucket in registers
+        // The sorted bucket written through LDS, kPermSlots slots per pass: every record goes to
+        // its slot's LDS entry, then the block writes the slots' five arrays with coalesced
+        // stores (a direct store per record and array scatters 4-byte words: 35 vs ~12 us at C3)
+        uint32_t lr[kRankRegs];
+#pragma unroll
+        for (int k = 0; k < kRankRegs; ++k)
+            lr[k] = bs + t + k * kRankThreads < be ? atomicAdd(&cnt[rec[k].x & lo_mask], 1u) : 0xFFFFFFFFu;
+        for (uint32_t p0 = 0; p0 < be - bs; p0 += kPermSlots) {
+#pragma unroll
+            for (int k = 0; k < kRankRegs; ++k)
+                if (lr[k] - p0 < (uint32_t)kPermSlots) {
+                    perm_rec[lr[k] - p0] = rec[k];
+                    perm_run[lr[k] - p0] = run[FIELDS ? k : 0];
+                }
+            __syncthreads();
+            for (uint32_t q = t; q < kPermSlots && p0 + q < be - bs; q += kRankThreads)
+                put(bs + p0 + q, perm_rec[q], perm_run[q]);
+            __syncthreads();
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kRankRegs; ++k)
         if (bs + t + k * kRankThreads < be) put(bs + atomicAdd(&cnt[rec[k].x & lo_mask], 1u), rec[k], run[FIELDS ? k : 0]);

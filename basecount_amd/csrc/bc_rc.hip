@@ -67,16 +67,16 @@ constexpr bool kEarlyWait = BC_RC_EARLY_WAIT != 0;
 #define BC_RC_GATHER 1
 #endif
 constexpr bool kGather = BC_RC_GATHER != 0;
-constexpr int kRcSlot = 76;  // stage bytes per read in gather staging (152 nibbles: 150-bp reads at either parity)
-static_assert(kRcSlot % 4 == 0 && kRcSlot * kRcChunk <= 78 * kRcChunk, "gather slots fit the stage");
-// Transposed gather staging (image chunks of a batch sorted on the device without moving its
-// sequence, bc_sort.hip's fields-only sort): each read's bytes from the 4-byte word holding its
-// first base, kGWords words, by LDS-DMA one word per lane (instruction e of a wave: word e of its
-// 64 reads, 256 contiguous LDS bytes), so the stage is [wave][word][lane]: a lane's words are 64
-// words apart and a wave reading one word of each of its reads hits 64 different banks, whatever
-// the reads' offsets (the linear stage's reads at unrelated offsets collide).
-constexpr int kGWords = 20;  // 80 bytes: a read of <= 77 bytes at any byte offset in its first word
-constexpr int kGStage = 4 * kGWords * kRcChunk;
+// Gather staging (chunks whose sequence is not one short segment: the reads of a batch sorted on
+// the device without moving its sequence, bc_sort.hip's fields-only sort): every simple read's
+// bytes, from the 4-byte word holding its first base, into its own kRcSlot-byte slot of the
+// stage by LDS-DMA.  The block's threads move the slots' words in stage order (instruction e of
+// wave w: stage words (20 w + e) * 64 + lane, ~3 reads' consecutive words), so an instruction
+// touches a handful of cache lines; one lane per read (each instruction 64 reads' lines) took
+// 122 us at C3 in random order, the register copy before it 220.
+constexpr int kRcSlot = 80;  // 20 words: a read of <= 77 bytes at any byte offset in its first word
+static_assert(kRcSlot == 80, "stage word -> slot by multiply-shift: (g * 3277) >> 16 == g / 20 for g < 5120");
+constexpr int kGStage = kRcSlot * kRcChunk;
 constexpr int kRcWinPos = 512;             // positions of the LDS histogram (one window pass)
 constexpr int kRcWin = kRcWinPos / 8;      // 8-position windows per pass
 
@@ -322,6 +322,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // image path, which overwrites both, uses neither (1 KiB of LDS kept for the gather stage:
     // a 512-byte larger block no longer fits three times into a CU, k_rc 46 -> 71 us at C3)
     int32_t* const rpos = (int32_t*)(rec + kRecU4);
+    // gather staging's per-read table (first word, words to move), past the read positions
+    uint32_t* const gtab = (uint32_t*)(rec + kRecAll);
+    static_assert(kRecAll * 16 + 8 * kRcReads <= (int)sizeof(rec), "the gather table fits the records region");
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[(kStage > kGStage ? kStage : kGStage) + 8 * kPadW];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
     __shared__ __attribute__((aligned(16))) uint32_t red[kRcWaves][8];
@@ -502,6 +505,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // v[7]: the longest simple read's sequence bytes (gather staging's slot test; not in the
         // upload's summaries, whose chunks never take gather staging)
         uint32_t v[8];
+        const uint32_t rbytes = ((msn & 1u) + T.qlen + 1u) >> 1;  // the read's sequence bytes
+        const bool over_slot = ((msn >> 1) & 3u) + rbytes > (uint32_t)kRcSlot;  // (gather staging: a complex read)
         const bool is_max[8] = {false, true, false, true, true, true, true, true};
         if (sums) {  // (uniform) reduced by the upload (bc_capi.hip chunk_summary: the same values)
             const uint32_t* sw = (const uint32_t*)elem(sums, 2 * chunk);
@@ -520,7 +525,12 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             // at its end) count as 3 runs: such a chunk takes the run tables
             v[5] = simple ? run_shape(T) : 0u;
             v[6] = (simple && T.gap) ? 1u : 0u;
-            v[7] = simple ? (((msn & 1u) + T.qlen + 1u) >> 1) : 0u;
+            v[7] = simple ? rbytes : 0u;
+            // gather staging's table, in case the chunk takes it (read before this chunk's records
+            // or image are written, past the records and read positions): the read's first word
+            // and the words to move (0: not gathered)
+            gtab[tid] = (msn >> 1) & ~3u;
+            gtab[kRcReads + tid] = (simple && !over_slot) ? (((msn >> 1) & 3u) + rbytes + 3u) >> 2 : 0u;
             RC_STAMP(1);
             block_reduce<8, kRcWaves>(v, is_max, red);  // contains a __syncthreads
             RC_STAMP(2);
@@ -551,20 +561,13 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const IT WBc = P0 & ~(IT)7;
         const int NWc = (int)(P1 > WBc ? (P1 - WBc + 7) / 8 : 0);
         const bool img_shape = maxrun <= 2 && NWc <= kImgRows && !(BC_ABL(A) & 8192);  // (uniform)
-        // an image chunk takes the transposed gather, a run-table chunk the linear slots
-        const bool gather_t = kGather && !QUAL && !staged && !sums && img_shape && v[7] <= 4u * kGWords - 3u &&
-                              !(BC_ABL(A) & 512);  // (uniform)
-        const bool gather = kGather && !QUAL && !staged && !sums && !gather_t && v[7] <= (uint32_t)kRcSlot &&
+        const bool gather = kGather && !QUAL && !staged && !sums && v[7] <= (uint32_t)kRcSlot &&
                             !(BC_ABL(A) & 512);  // (uniform)
-        const uint32_t rbytes = ((msn & 1u) + T.qlen + 1u) >> 1;  // the read's sequence bytes
-        const bool big = simple && ((gather && rbytes > (uint32_t)kRcSlot) ||
-                                    (gather_t && ((msn >> 1) & 3u) + rbytes > 4u * kGWords));
+        const bool big = gather && simple && over_slot;
         const bool cxa = cx || big, simplea = simple && !big;
-        const bool inlds = staged || gather || gather_t;  // (uniform) the walks read the stage
-        // the read's first base as a nibble index of the stage (or of the batch's buffer); in the
-        // transposed stage, of the read's own column
-        const uint32_t rel = gather_t ? (msn & 7u)
-                             : gather ? (uint32_t)(2 * kRcSlot * tid) + (msn & 1u) : msn - (staged ? 2u * seg_lo : 0u);
+        const bool inlds = staged || gather;  // (uniform) the walks read the stage
+        // the read's first base as a nibble index of the stage (or of the batch's buffer)
+        const uint32_t rel = gather ? (uint32_t)(2 * kRcSlot * tid) + (msn & 7u) : msn - (staged ? 2u * seg_lo : 0u);
         if (cxa) cxl[atomicAdd(&ncx[par], 1u)] = (uint32_t)tid;
         const bool img_path = inlds && img_shape;
         const int gpad = NWc;  // (uniform) the image's group padding (see rec)
@@ -602,31 +605,16 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 *(uint4*)(stage + off) = q4;
             }
         }
-        if (gather_t && simplea) {
-            // the read's words (from the one holding its first base) into its column of the
-            // wave's [word][lane] block: word e of every read of the wave is one LDS-DMA
-            // instruction (a lane's address; the destination 64 consecutive words)
-            const uint8_t* src = A.seq + ((msn >> 1) & ~3u);
-            const uint32_t nw = (((msn >> 1) & 3u) + rbytes + 3u) >> 2;
-            uint8_t* dst = stage + wave * (4 * 64 * kGWords);
-#pragma unroll
-            for (int e = 0; e < kGWords; ++e)
-                if ((uint32_t)e < nw)
-                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 4 * e), (lds_void_t*)(dst + 256 * e), 4, 0, 0);
-        }
-        if (gather && simplea) {
-            // the read's bytes from its first base on, 4-byte words funnel-shifted from the aligned
-            // words around them (up to 7 bytes past the read: the buffer is padded), into its slot
-            const uint32_t from = msn >> 1, nw = ((((msn & 1u) + T.qlen + 1u) >> 1) + 3u) >> 2;
-            const uint32_t* s32 = (const uint32_t*)(A.seq + (from & ~3u));
-            const uint32_t sh = (from & 3u) * 8u;
-            uint32_t* d32 = (uint32_t*)(stage + kRcSlot * tid);
-            uint32_t wv[kRcSlot / 4 + 1];
-#pragma unroll
-            for (int w = 0; w <= kRcSlot / 4; ++w) wv[w] = (uint32_t)w <= nw ? s32[w] : 0u;
-#pragma unroll
-            for (int w = 0; w < kRcSlot / 4; ++w)
-                if ((uint32_t)w < nw) d32[w] = __builtin_amdgcn_alignbit(wv[w + 1], wv[w], sh);
+        if (gather) {  // (uniform) the slots' words in stage order, a few reads per instruction
+            // (not unrolled: the 40 table reads of an unrolled loop, hoisted together, spill)
+#pragma unroll 1
+            for (int e = 0; e < kRcSlot / 4; ++e) {
+                const uint32_t g = (uint32_t)((wave * (kRcSlot / 4) + e) * 64 + lane);  // stage word
+                const uint32_t r = (g * 3277u) >> 16, k = g - (uint32_t)(kRcSlot / 4) * r;  // slot r, word k
+                if (k < gtab[kRcReads + r])
+                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(A.seq + gtab[r] + 4u * k),
+                                                     (lds_void_t*)(stage + 256 * (wave * (kRcSlot / 4) + e)), 4, 0, 0);
+            }
         }
         // ---- records (pos kept for complex / padding entries so pos[] stays sorted)
         {
@@ -668,25 +656,16 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             // run k's stage word of row r is f_k + r (+1 for the funnel's upper word): within
             // [-kPadW + 1, kStage / 4 + kPadW - 1] for every simple read (f_k >= -1 - 22, the
             // read's sequence lies in the stage), so the stage's pads absorb it unclamped
-            // run k's stage word for row r: w_k[r * S] (S = 1: the linear stage; S = 64: the
-            // transposed gather stage, the lane's column of its wave's [word][lane] block; rows
-            // outside the read read words that the masks discard)
-            auto colp = [&](int wb, auto st_c) -> const uint32_t* {
-                constexpr int S = decltype(st_c)::value;
-                return S == 1 ? (const uint32_t*)stage + (wb - i0)
-                              : (const uint32_t*)stage + wave * (64 * kGWords) + lane + 64 * (wb - i0);
-            };
+            const uint32_t* w0 = (const uint32_t*)stage + (wb0 - i0);
+            const uint32_t* w1 = (const uint32_t*)stage + (wb1 - i0);
             // Row r's 8 event classes, all rows unrolled without branches so the LDS reads of
             // later rows issue ahead.  ge(X): the row's stream bits at or above X, i.e. bits
             // >= d = clamp(X - 32r, 0, 32).  The clamp is one med3 of X against [32r, 32r + 32]
             // (constants the compiler keeps in registers), and 0xFFFFFFFF << (m mod 64) as 64
             // bits holds the mask in its low word (even r: m mod 64 = d) or its high word (odd r:
             // 32 + d, or 0 when d = 32).
-            auto expand = [&](auto two_c, auto edge_c, auto st_c) {
+            auto expand = [&](auto two_c, auto edge_c) {
                 constexpr bool TWO = decltype(two_c)::value, EDGE = decltype(edge_c)::value;
-                constexpr int S = decltype(st_c)::value;
-                const uint32_t* w0 = colp(wb0, st_c);
-                const uint32_t* w1 = colp(wb1, st_c);
                 const int yz = Z, yb = B0e, ya = A1, ys = SP;
                 uint32_t p0 = w0[0], p1 = TWO ? w1[0] : 0u;
 #pragma unroll
@@ -699,12 +678,12 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                         return (row & 1) ? (uint32_t)(v >> 32) : (uint32_t)v;
                     };
                     const uint32_t gz = ge(yz), gb = ge(yb);
-                    const uint32_t n0 = w0[(row + 1) * S];
+                    const uint32_t n0 = w0[row + 1];
                     uint32_t x = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n0, p0, sh0), gz, gb, 0x40);
                     p0 = n0;
                     if (TWO) {
                         const uint32_t ga = ge(ya), gs = ge(ys);
-                        const uint32_t n1 = w1[(row + 1) * S];
+                        const uint32_t n1 = w1[row + 1];
                         const uint32_t x1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(n1, p1, sh1), ga, gs, 0x40);
                         // (independent terms: a select chain measured slower, 57 vs 54 us)
                         // s0 & s1 & ~s2 (0x40); then s0 | s1 | s2 (0xFE) in one op
@@ -734,16 +713,13 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 const int lo = (a + 31) >> 5, hi = b >> 5;
                 return hi > lo ? lo32_bit(hi) - lo32_bit(lo) : 0u;
             };
-            auto interior = [&](auto st_c) {
-                constexpr int S = decltype(st_c)::value;
-                const uint32_t* w0 = colp(wb0, st_c);
-                const uint32_t* w1 = colp(wb1, st_c);
+            auto interior = [&]() {
                 const uint32_t o0 = rowmask(Z, B0e), o1 = rowmask(A1, SP);
                 uint32_t p0 = w0[0], p1 = w1[0];
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) {
                     if (row >= kImgRows - 4 && row >= NWc) continue;  // (uniform) past the chunk
-                    const uint32_t n0 = w0[(row + 1) * S], n1 = w1[(row + 1) * S];
+                    const uint32_t n0 = w0[row + 1], n1 = w1[row + 1];
                     const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)o0, row, 1);
                     const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)o1, row, 1);
                     const uint32_t x1 = __builtin_amdgcn_alignbit(n1, p1, sh1) & m1;
@@ -767,8 +743,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                     for (int k = 0; k < 4; ++k) {
                         const int rb = bs[k] >> 5;
                         rbs[k] = rb < kImgRows - 1 ? rb : kImgRows - 1;
-                        q0[k] = make_uint2(w0[rbs[k] * S], w0[(rbs[k] + 1) * S]);
-                        q1[k] = make_uint2(w1[rbs[k] * S], w1[(rbs[k] + 1) * S]);
+                        q0[k] = make_uint2(w0[rbs[k]], w0[rbs[k] + 1]);
+                        q1[k] = make_uint2(w1[rbs[k]], w1[rbs[k] + 1]);
                     }
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
@@ -789,12 +765,9 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
 #pragma unroll
                 for (int row = 0; row < kImgRows; ++row) mycol[row] = 0u;
             } else if (8 * (IT)(G0 + kImgRows) > L) {  // (uniform) rows may reach past L
-                if (gather_t) expand(std::true_type{}, std::true_type{}, std::integral_constant<int, 64>{});
-                else expand(std::true_type{}, std::true_type{}, std::integral_constant<int, 1>{});
-            } else if (gather_t) {  // (uniform)
-                interior(std::integral_constant<int, 64>{});
+                expand(std::true_type{}, std::true_type{});
             } else {
-                interior(std::integral_constant<int, 1>{});
+                interior();
             }
         }
         pf_ok = false;

@@ -325,6 +325,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // gather staging's per-read table (first word, words to move), past the read positions
     uint32_t* const gtab = (uint32_t*)(rec + kRecAll);
     static_assert(kRecAll * 16 + 8 * kRcReads <= (int)sizeof(rec), "the gather table fits the records region");
+    // (the gather stage's slots reach kGStage bytes; both layouts keep kPadW words of pad after)
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[(kStage > kGStage ? kStage : kGStage) + 8 * kPadW];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
     __shared__ __attribute__((aligned(16))) uint32_t red[kRcWaves][8];
@@ -791,7 +792,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             pf_ok = true;
         }
         const SeqSrc src{inlds ? (const uint32_t*)stage : (const uint32_t*)A.seq,
-                         inlds ? (int64_t)(kStage / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
+                         inlds ? (int64_t)((gather ? kGStage : kStage) / 4) : A.seq_words, A.qual, A.qual_bytes, A.mbq};
         const IT WB = P0 & ~(IT)7;
         const int G0w = (int)(WB >> 3);  // the image's first window (image path)
         const IT NW = P1 > WB ? (P1 - WB + 7) / 8 : 0;

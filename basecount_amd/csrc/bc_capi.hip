@@ -727,6 +727,22 @@ int bc_pileup_summary(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int
                       int32_t* d_counts, int32_t* d_cov, double* d_pc, double* d_ent, double* d_sec, void* d_work,
                       double* d_out) {
     if (!d_out) return fail(BC_E_ARG, "NULL argument");
+    if (c && r && d_work && L > 0 && !d_pc && bc::use_rc(*r, L, c->shape) && (k == 5 || k == 6)) {
+        // a deep batch: kernel 2 leaves numpy's leaf partials and ONE launch folds them (the fused
+        // tail of bc_pileup_summary_amplicons, no windows); summary only: context stand-ins
+        if (!d_counts && !d_cov && !d_ent && !d_sec) {
+            const size_t need = (size_t)L * (4u * (size_t)k + 4u + 16u);
+            DeviceGuard g(c->device);
+            if (int rc = out_scratch(c, need)) return rc;
+            d_ent = (double*)c->out_scratch;
+            d_sec = d_ent + L;
+            d_cov = (int32_t*)(d_sec + L);
+            d_counts = d_cov + L;
+        }
+        if (d_counts && d_cov && d_ent && d_sec)
+            return bc_pileup_summary_amplicons(c, r, L, mbq, k, nf, nf2, d_counts, d_cov, d_ent, d_sec, d_work, d_out,
+                                               nullptr, nullptr, 0, nullptr);
+    }
     int rc = bc_pileup_partials(c, r, L, mbq, k, nf, nf2, d_counts, d_cov, d_pc, d_ent, d_sec, d_work);
     if (rc) return rc;
     return bc_summary_fold(c, 1, &L, &d_work, &d_out);
@@ -876,6 +892,54 @@ int bc_amplicons(bc_ctx* c, const int32_t* d_cov, const double* d_ent, const dou
     DeviceGuard g(c->device);
     Timed tm(c, BC_K_AMPLICONS);
     HIP_TRY(bc::launch_amplicons(c->stream, d_cov, d_ent, d_sec, L, d_lo, d_hi, n_tiles, d_out));
+    return BC_OK;
+}
+
+int bc_pileup_summary_amplicons(bc_ctx* c, const bc_reads* r, int64_t L, uint32_t mbq, int k, double nf, double nf2,
+                                int32_t* d_counts, int32_t* d_cov, double* d_ent, double* d_sec, void* d_work,
+                                double* d_out, const int64_t* d_lo, const int64_t* d_hi, int32_t n_tiles,
+                                double* d_amp) {
+    if (!c || !r || !d_work || !d_out) return fail(BC_E_ARG, "NULL argument");
+    if (L <= 0) return fail(BC_E_ARG, "ref_len must be > 0 (np.mean of an empty list)");
+    if (n_tiles < 0) return fail(BC_E_ARG, "n_tiles < 0");
+    if (n_tiles > 0 && (!d_lo || !d_hi || !d_amp)) return fail(BC_E_ARG, "NULL window argument");
+    if (!d_counts || !d_cov || !d_ent || !d_sec) return fail(BC_E_ARG, "NULL output");
+    if (!bc::use_rc(*r, L, c->shape)) {  // shallow batches: the fused sweeps, then the windows
+        int rc = bc_pileup_summary(c, r, L, mbq, k, nf, nf2, d_counts, d_cov, nullptr, d_ent, d_sec, d_work, d_out);
+        if (rc) return rc;
+        return bc_amplicons(c, d_cov, d_ent, d_sec, L, d_lo, d_hi, n_tiles, d_amp);
+    }
+    // the argument checks of bc_pileup
+    if (k != 5 && k != 6) return fail(BC_E_ARG, "k must be 5 or 6");
+    if (!r->sorted) return fail(BC_E_ARG, "bc_pileup needs a coordinate-sorted batch (sorted == 1)");
+    if (mbq > 0 && r->n_reads > 0 && !r->qual) return fail(BC_E_ARG, "min_base_quality > 0 needs qualities");
+    if (r->n_reads > 0 && r->seq_layout != BC_SEQ_EVENT)
+        return fail(BC_E_ARG, "bc_pileup needs seq_layout == BC_SEQ_EVENT (see bc_seq_to_event)");
+    if (r->n_reads > 0 && ((uintptr_t)r->seq & 15u))
+        return fail(BC_E_ARG, "bc_pileup needs a 16-byte aligned sequence buffer");
+    DeviceGuard g(c->device);
+    const size_t need = (size_t)k * (size_t)L * 4;
+    if (need > c->rc_scratch_bytes) {  // as bc_pileup: grow-only, kept zeroed by kernel 2
+        if (c->rc_scratch) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipFree(c->rc_scratch));
+            c->rc_scratch = nullptr;
+            c->rc_scratch_bytes = 0;
+        }
+        HIP_TRY(hipMalloc((void**)&c->rc_scratch, need));
+        c->rc_scratch_bytes = need;
+        HIP_TRY(hipMemsetAsync(c->rc_scratch, 0, need, c->stream));
+    }
+    {
+        Timed tm(c, BC_K_RC);
+        HIP_TRY(bc::launch_rc(c->stream, *r, L, mbq, k, c->rc_scratch, c->d_err));
+    }
+    {
+        Timed tm(c, BC_K_STATS);
+        HIP_TRY(bc::launch_stats_leaves(c->stream, c->rc_scratch, L, k, nf, nf2, d_cov, d_ent, d_sec, d_counts, d_work));
+    }
+    Timed tm(c, BC_K_AMPLICONS);
+    HIP_TRY(bc::launch_tail(c->stream, d_cov, d_ent, d_sec, L, d_work, d_out, d_lo, d_hi, n_tiles, d_amp));
     return BC_OK;
 }
 

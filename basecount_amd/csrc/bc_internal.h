@@ -160,5 +160,13 @@ hipError_t launch_summary_fold(hipStream_t s, int n, const int64_t* L, void* con
 SumParts summary_parts(void* work, int64_t L);
 hipError_t launch_amplicons(hipStream_t s, const int32_t* cov, const double* ent, const double* sec,
                             int64_t L, const int64_t* lo, const int64_t* hi, int n_tiles, double* out);
+// The fused --summarise-with-bed tail (bc_pileup_summary_amplicons): kernel 2 that also writes
+// numpy's 128-position leaf partials into the summary work buffer, then ONE launch for the
+// summary (out: mean coverage, mean entropy, non-zero positions, coverage sum) and every
+// amplicon window (amp: 6 doubles per window)
+hipError_t launch_stats_leaves(hipStream_t s, int32_t* hist, int64_t L, int k, double nf, double nf2, int32_t* cov,
+                               double* ent, double* sec, int32_t* counts_out, void* work);
+hipError_t launch_tail(hipStream_t s, const int32_t* cov, const double* ent, const double* sec, int64_t L, void* work,
+                       double* out, const int64_t* lo, const int64_t* hi, int n_tiles, double* amp);
 
 }  // namespace bc

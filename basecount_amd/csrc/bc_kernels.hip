@@ -343,11 +343,22 @@ __global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, in
 // the counts' load (issued before the table copy, so both are in flight together), the fp64
 // terms and the stores.  The arithmetic is bc_stats.h's position_stats (the fused kernels'), so the
 // results are those of k_stats bit for bit; NULL cov / pc / ent / sec are skipped as in k_stats.
-template <int K>
+// LEAVES (the fused --summarise-with-bed tail, launch_stats_leaves): the block's 256 positions
+// are two of numpy's 128-position pairwise leaves when they lie in a whole 8192-position buffer,
+// and the block also writes each leaf's entropy sum (eight strided accumulators, added in
+// numpy's order), its exact coverage sum and its non-zero count, so no summary pass re-reads
+// the entropies (k_tail adds the leaves up the buffer's tree).
+struct Leaves {
+    double* ent;  // [full buffers * 64]
+    long long* cov;
+    long long* nz;
+    int64_t full;  // positions in whole 8192-position buffers
+};
+template <int K, bool LEAVES = false>
 __global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, int64_t L, double nf, double nf2,
                                                     int32_t* __restrict__ counts_out, int32_t* __restrict__ cov_out,
                                                     double* __restrict__ pc, double* __restrict__ ent,
-                                                    double* __restrict__ sec) {
+                                                    double* __restrict__ sec, Leaves lv = Leaves{}) {
     __shared__ __attribute__((aligned(16))) double tab[64][4];
     const int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const bool in = P < L;
@@ -358,8 +369,8 @@ __global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, 
         *(double2*)&tab[threadIdx.x >> 1][2 * (threadIdx.x & 1)] =
             *(const double2*)&log2d::kTab[threadIdx.x >> 1][2 * (threadIdx.x & 1)];
     __syncthreads();
-    if (!in) return;
-    if (counts_out) {
+    if (!in && !LEAVES) return;
+    if (counts_out && in) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             counts_out[(int64_t)j * L + P] = (int32_t)c[j];
@@ -374,7 +385,7 @@ __global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, 
         cov += c[j];
         if (c[j] > mx) mx = c[j], am = j;  // np.argmax: first maximum
     }
-    if (cov_out) cov_out[P] = (int32_t)cov;
+    if (cov_out && in) cov_out[P] = (int32_t)cov;
     double h = 1.0, h2 = 1.0;
     if (cov != 0) {
         double s = 0.0;
@@ -396,12 +407,42 @@ __global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, 
                 }
             h2 = nf2 * s2;
         }
-    } else if (pc) {
+    } else if (pc && in) {
 #pragma unroll
         for (int j = 0; j < K; ++j) pc[(int64_t)j * L + P] = -1.0;
     }
-    if (ent) ent[P] = h;
-    if (sec) sec[P] = h2;
+    if (in) {
+        if (ent) ent[P] = h;
+        if (sec) sec[P] = h2;
+    }
+    if (LEAVES && (int64_t)blockIdx.x * 256 + 256 <= lv.full) {  // (uniform) two whole leaves
+        __shared__ double s_h[256];
+        __shared__ long long s_r[8];
+        const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+        s_h[t] = h;
+        long long cs = cov, nzc = cov != 0;
+        for (int o = 32; o > 0; o >>= 1) {
+            cs += __shfl_down(cs, o);
+            nzc += __shfl_down(nzc, o);
+        }
+        if (lane == 0) s_r[wave] = cs, s_r[4 + wave] = nzc;
+        __syncthreads();
+        if (t < 16) {  // leaf t >> 3, accumulator j = t & 7: r_j = a[j] + a[j + 8] + ... in order
+            const double* a = s_h + 128 * (t >> 3) + (t & 7);
+            double r = a[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) r += a[8 * i];
+            r = r + __shfl_down(r, 1);  // (r0+r1), (r2+r3), ...
+            r = r + __shfl_down(r, 2);  // (r0+r1)+(r2+r3), (r4+r5)+(r6+r7)
+            r = r + __shfl_down(r, 4);  // the leaf
+            if ((t & 7) == 0) {
+                const int64_t f = (int64_t)blockIdx.x * 2 + (t >> 3);
+                lv.ent[f] = r;
+                lv.cov[f] = s_r[2 * (t >> 3)] + s_r[2 * (t >> 3) + 1];
+                lv.nz[f] = s_r[4 + 2 * (t >> 3)] + s_r[4 + 2 * (t >> 3) + 1];
+            }
+        }
+    }
 }
 
 // Kernel 2 with eight lanes per position: lane j < K computes column j's percentage and its two
@@ -1133,6 +1174,149 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
     }
 }
 
+// ---- the fused --summarise-with-bed tail (main.py:469-551) after kernel 1 + 2 -------------------
+// One launch: blocks [0, 3 n_tiles) take one (amplicon window, array) each -- array 0 coverage,
+// 1 entropy, 2 secondary entropy: its numpy mean and np.median -- and the last block the summary:
+// every whole buffer's 64 leaves (k_stats_lane<LEAVES>) added up numpy's tree by a wave, the
+// buffers folded in order, the last partial buffer's pairwise sum from LDS (pw_block), the exact
+// coverage sum and non-zero count.  The windows' medians: a window of <= 512 positions is staged
+// in LDS and each element's rank is counted against all of them (ties by index: the sorted
+// order's position, exact), so the elements of rank (n-1)/2 and n/2 are the middle ones; longer
+// windows take the radix select.  Same values as k_amplicon + k_sum_chunks + k_sum_final.
+constexpr int kTailWin = 512;
+__global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* ent, const double* sec, int64_t L,
+                                              const int64_t* lo_a, const int64_t* hi_a, int n_tiles, double* amp,
+                                              Leaves lv, double* out) {
+    __shared__ unsigned s_hist[256];
+    __shared__ unsigned long long s_sel[2];
+    __shared__ long long s_red[8];
+    __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
+    __shared__ double s_val[2 << kLv];
+    __shared__ unsigned long long s_key[kTailWin];
+    __shared__ double s_buf[4];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if ((int)blockIdx.x == 3 * n_tiles) {  // (uniform) the summary
+        const int64_t nfull = lv.full / kNpBuf;
+        double s = 0.0;
+        long long cs = 0, nz = 0;
+        for (int64_t b0 = 0; b0 < nfull; b0 += 4) {
+            const int64_t b = b0 + wave;
+            double v = 0.0;
+            if (b < nfull) {
+                const int64_t f = b * 64 + lane;
+                v = lv.ent[f];
+                cs += lv.cov[f];
+                nz += lv.nz[f];
+            }
+            // numpy's tree over a buffer's 64 leaves: neighbours first (pw_full8192's order)
+            v = v + __shfl_down(v, 1);
+            v = v + __shfl_down(v, 2);
+            v = v + __shfl_down(v, 4);
+            v = v + __shfl_down(v, 8);
+            v = v + __shfl_down(v, 16);
+            v = v + __shfl_down(v, 32);
+            if (lane == 0) s_buf[wave] = v;
+            __syncthreads();
+            if (t == 0)
+                for (int w = 0; w < 4 && b0 + w < nfull; ++w) s += s_buf[w];  // buffers in order
+            __syncthreads();
+        }
+        const int m = (int)(L - lv.full);  // the last, partial buffer: [full, L)
+        if (m > 0) {
+            extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+            double* s_ent = (double*)dyn;
+            for (int i = t; i < m; i += 256) {
+                const int32_t c = cov[lv.full + i];
+                s_ent[i] = ent[lv.full + i];
+                cs += c;
+                nz += c != 0;
+            }
+            __syncthreads();
+            const double e = pw_block(s_ent, m, s_off, s_len, s_val);
+            if (t == 0) s += e;
+        }
+        cs = block_sum_i64(cs, s_red);
+        nz = block_sum_i64(nz, s_red);
+        if (t == 0) {
+            const double n = (double)L;
+            out[0] = (double)cs / n;  // integer sum exact in float64 below 2^53: np.mean == sum / n
+            out[1] = s / n;
+            out[2] = (double)nz;
+            out[3] = (double)cs;
+        }
+        return;
+    }
+    const int w = (int)blockIdx.x / 3, q = (int)blockIdx.x % 3;
+    int64_t lo = lo_a[w], hi = hi_a[w];
+    if (lo < 0) lo = 0;
+    if (hi > L - 1) hi = L - 1;
+    double* o = amp + (int64_t)w * 6 + 2 * q;
+    if (lo > hi) {
+        if (t == 0) o[0] = o[1] = -1.0;
+        return;
+    }
+    const int64_t n = hi - lo + 1;
+    const int64_t k1 = (n - 1) / 2, k2 = n / 2;
+    // keys that order like the values: the coverage as an unsigned int, the entropies (>= 0) by
+    // their bit patterns
+    auto key = [&](int64_t i) -> unsigned long long {
+        return q == 0 ? (unsigned long long)(uint32_t)cov[lo + i]
+                      : (unsigned long long)__double_as_longlong((q == 1 ? ent : sec)[lo + i]);
+    };
+    unsigned long long a, b;
+    double mean;
+    if (n <= kTailWin) {  // (uniform)
+        for (int i = t; i < n; i += 256) s_key[i] = key(i);
+        __syncthreads();
+        // ranks of elements t and t + 256: #smaller + #equal before it
+        const int i0 = t, i1 = t + 256;
+        const unsigned long long x0 = i0 < n ? s_key[i0] : 0ull, x1 = i1 < n ? s_key[i1] : 0ull;
+        int r0 = 0, r1 = 0;
+        for (int j = 0; j < n; ++j) {
+            const unsigned long long y = s_key[j];  // (one address per wave: a broadcast)
+            r0 += (y < x0 || (y == x0 && j < i0)) ? 1 : 0;
+            r1 += (y < x1 || (y == x1 && j < i1)) ? 1 : 0;
+        }
+        if (i0 < n && r0 == k1) s_sel[0] = x0;
+        if (i0 < n && r0 == k2) s_sel[1] = x0;
+        if (i1 < n && r1 == k1) s_sel[0] = x1;
+        if (i1 < n && r1 == k2) s_sel[1] = x1;
+        if (q == 0) {  // (uniform) the exact integer sum
+            long long cs = 0;
+            for (int i = t; i < n; i += 256) cs += (long long)s_key[i];
+            cs = block_sum_i64(cs, s_red);  // (contains the barriers after the rank writes)
+            mean = (double)cs / (double)n;
+        } else {  // numpy's pairwise mean over the window (values in LDS, as doubles)
+            __syncthreads();
+            mean = pw_block((const double*)s_key, (int)n, s_off, s_len, s_val) / (double)n;
+        }
+        a = s_sel[0];
+        b = s_sel[1];
+    } else {  // a long window: radix selects
+        const int bits = q == 0 ? 32 : 64;
+        a = radix_select(key, n, k1, bits, s_hist, s_sel);
+        b = k2 != k1 ? radix_select(key, n, k2, bits, s_hist, s_sel) : a;
+        if (q == 0) {
+            long long cs = 0;
+            for (int64_t i = t; i < n; i += 256) cs += (long long)(uint32_t)cov[lo + i];
+            cs = block_sum_i64(cs, s_red);
+            mean = (double)cs / (double)n;
+        } else {
+            mean = np_mean_block((q == 1 ? ent : sec) + lo, n, s_off, s_len, s_val);
+        }
+    }
+    if (t == 0) {
+        o[0] = mean;
+        if (q == 0) {
+            const double ca = (double)a, cb = (double)b;
+            o[1] = (k2 != k1) ? ((0.0 + ca) + cb) / 2.0 : ca;
+        } else {
+            const double va = __longlong_as_double((long long)a), vb = __longlong_as_double((long long)b);
+            o[1] = (k2 != k1) ? ((0.0 + va) + vb) / 2.0 : (0.0 + va) / 1.0;
+        }
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------ launchers
@@ -1231,7 +1415,43 @@ hipError_t launch_stats(hipStream_t s, const int32_t* hist, int64_t L, int k, do
 
 size_t summary_work_bytes(int64_t L) {
     const int64_t nc = (L + kNpBuf - 1) / kNpBuf;
-    return 16 + (size_t)(nc > 0 ? nc : 1) * 24 * 5;  // header; per buffer: its partials + its 4 quarters'
+    // header; per buffer: its partials + its 4 quarters', and its 64 leaves' (the fused tail)
+    return 16 + (size_t)(nc > 0 ? nc : 1) * (24 * 5 + 24 * 64);
+}
+
+// the leaf partials inside a summary work buffer (after the buffer and quarter partials)
+static Leaves summary_leaves(void* work, int64_t L) {
+    const int64_t nc = (L + kNpBuf - 1) / kNpBuf, m = nc > 0 ? nc : 1;
+    Leaves lv;
+    lv.ent = (double*)((uint8_t*)work + 16 + (size_t)m * 24 * 5);
+    lv.cov = (long long*)(lv.ent + 64 * m);
+    lv.nz = lv.cov + 64 * m;
+    lv.full = (L / kNpBuf) * kNpBuf;
+    return lv;
+}
+
+hipError_t launch_stats_leaves(hipStream_t s, int32_t* hist, int64_t L, int k, double nf, double nf2, int32_t* cov,
+                               double* ent, double* sec, int32_t* counts_out, void* work) {
+    if (L <= 0) return hipSuccess;
+    const Leaves lv = summary_leaves(work, L);
+    const unsigned lb = (unsigned)((L + 255) / 256);
+    if (k == 5)
+        hipLaunchKernelGGL((k_stats_lane<5, true>), dim3(lb), dim3(256), 0, s, hist, L, nf, nf2, counts_out, cov,
+                           nullptr, ent, sec, lv);
+    else
+        hipLaunchKernelGGL((k_stats_lane<6, true>), dim3(lb), dim3(256), 0, s, hist, L, nf, nf2, counts_out, cov,
+                           nullptr, ent, sec, lv);
+    return hipGetLastError();
+}
+
+hipError_t launch_tail(hipStream_t s, const int32_t* cov, const double* ent, const double* sec, int64_t L, void* work,
+                       double* out, const int64_t* lo, const int64_t* hi, int n_tiles, double* amp) {
+    if (L <= 0) return hipSuccess;
+    const Leaves lv = summary_leaves(work, L);
+    const size_t tail_lds = (size_t)(L - lv.full) * sizeof(double);
+    hipLaunchKernelGGL(k_tail, dim3((unsigned)(3 * n_tiles + 1)), dim3(256), tail_lds, s, cov, ent, sec, L, lo, hi,
+                       n_tiles, amp, lv, out);
+    return hipGetLastError();
 }
 
 SumParts summary_parts(void* work, int64_t L) {

@@ -363,6 +363,13 @@ constexpr int kBktChunk = 4096;    // reads per count / scatter block aimed at
 constexpr int kBktLowMax = 4096;   // low-bit bins of one bucket (2^12)
 constexpr uint32_t kQlenMax = 0xFFFFu;  // query lengths packed in 16 bits
 constexpr int64_t kSortCapMax = 0x55555550;  // room = 1.5 cap < 2^31: nibble indices 2 * room fit 32 bits
+// fields-only sorts: run records from the scatter's CIGAR loads (k_rc then loads a record per read
+// instead of the read's CIGAR, which in a sorted view of an unsorted batch lies anywhere);
+// -DBC_SORT_RUNS=0 builds the A/B variant without them (no CIGAR loads in the sort at all)
+#ifndef BC_SORT_RUNS
+#define BC_SORT_RUNS 1
+#endif
+constexpr bool kSortRuns = BC_SORT_RUNS != 0;
 constexpr uint32_t kBigRec = 0xFFFFFFFFu;  // record word 3 of a read whose fields need 32 bits: word 2 = its index
 
 __device__ __forceinline__ uint32_t bkt_pos(const SortArgs& A, int64_t i, bool& bad) {
@@ -508,6 +515,15 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
                 sn[u] = A.seq_nib[i];
             }
         }
+        if (FIELDS && !kSortRuns) {  // the record alone
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const int64_t i = i0 + (int64_t)u * kBktThreads;
+                if (i >= end) break;
+                A.brec[atomicAdd(&next[p[u] >> A.wbits], 1u)] = make_uint4(p[u], cb[u], sn[u], cn[u]);
+            }
+            continue;
+        }
         uint32_t w[B][8];
 #pragma unroll
         for (int u = 0; u < B; ++u)
@@ -585,7 +601,7 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     for (int k = 0; k < kRankRegs; ++k) {
         const uint32_t r = bs + t + k * kRankThreads;
         rec[k] = r < be ? A.brec[r] : make_uint4(0u, 0u, 0u, 0u);
-        if (FIELDS) run[k] = r < be ? A.brun[r] : make_uint4(0u, 0u, 0u, 0u);
+        if (FIELDS && kSortRuns) run[k] = r < be ? A.brun[r] : make_uint4(0u, 0u, 0u, 0u);
     }
     // the record of sorted slot j: its start-ordered copy (srec), or with FIELDS the sorted
     // batch's own arrays (the sequence stays where it is: seq_nib is the source's)
@@ -595,7 +611,7 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
             A.o_cig_beg[j] = x.y;
             A.o_seq_nib[j] = x.z;
             A.o_cig_n[j] = x.w;
-            A.o_runs[j] = y;
+            if (kSortRuns) A.o_runs[j] = y;
         } else {
             A.srec[j] = x;
         }
@@ -648,7 +664,7 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
             for (int k = 0; k < kRankRegs; ++k)
                 if (lr[k] - p0 < (uint32_t)kPermSlots) {
                     perm_rec[lr[k] - p0] = rec[k];
-                    perm_run[lr[k] - p0] = run[FIELDS ? k : 0];
+                    if (kSortRuns) perm_run[lr[k] - p0] = run[FIELDS ? k : 0];
                 }
             __syncthreads();
             for (uint32_t q = t; q < kPermSlots && p0 + q < be - bs; q += kRankThreads)
@@ -662,7 +678,7 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
         if (bs + t + k * kRankThreads < be) put(bs + atomicAdd(&cnt[rec[k].x & lo_mask], 1u), rec[k], run[FIELDS ? k : 0]);
     for (uint32_t r = more + t; r < be; r += kRankThreads) {
         const uint4 x = A.brec[r];
-        put(bs + atomicAdd(&cnt[x.x & lo_mask], 1u), x, FIELDS ? A.brun[r] : x);
+        put(bs + atomicAdd(&cnt[x.x & lo_mask], 1u), x, (FIELDS && kSortRuns) ? A.brun[r] : x);
     }
 }
 
@@ -854,11 +870,11 @@ hipError_t launch_sort(hipStream_t s, const bc_reads& r, bc_reads& out, void* me
         out.seq_nib = A.o_seq_nib;
         out.sorted = 1;
         out.seq_layout = BC_SEQ_EVENT;
-        out.read_runs = (const uint32_t*)A.o_runs;
+        out.read_runs = kSortRuns ? (const uint32_t*)A.o_runs : nullptr;
         out.run_chunks = 0;
         out.tile_reads = nullptr;
         out.n_tiles = 0;
-        out.index_tag = index_tag(out);
+        out.index_tag = kSortRuns ? index_tag(out) : 0;
         return hipSuccess;
     }
     out.pos = A.o_pos;

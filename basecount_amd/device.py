@@ -91,6 +91,8 @@ def lib() -> C.CDLL:
         "bc_seq_to_event": ([vp, vp, i64, vp], C.c_int),
         "bc_summary": ([vp, vp, vp, i64, vp, vp], C.c_int),
         "bc_amplicons": ([vp, vp, vp, vp, i64, vp, vp, C.c_int32, vp], C.c_int),
+        "bc_pileup_summary_amplicons": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, dbl, dbl, vp, vp, vp, vp, vp, vp,
+                                         vp, vp, C.c_int32, vp], C.c_int),
         "bc_bcount_host": ([C.c_int, i64, u32, C.POINTER(BcReads), vp, C.POINTER(i64),
                             C.POINTER(i64)], C.c_int),
         "bc_pileup": ([vp, C.POINTER(BcReads), i64, u32, C.c_int, dbl, dbl, vp, vp, vp, vp, vp],
@@ -396,6 +398,16 @@ class Context:
 
     def summary(self, d_cov, d_ent, L, d_work, d_out) -> None:
         check(lib().bc_summary(self.h, d_cov, d_ent, int(L), d_work, d_out))
+
+    def pileup_summary_amplicons(self, reads, L, mbq, k, nf, nf2, d_counts, d_cov, d_ent, d_sec, d_work, d_out,
+                                 d_lo, d_hi, n_tiles, d_amp) -> None:
+        """bc_pileup_summary_amplicons: --summarise-with-bed for one reference (the summary's 4
+        doubles into d_out, 6 per amplicon window into d_amp); a deep batch's tail after kernel 1
+        is kernel 2 + ONE launch."""
+        r = reads.r if isinstance(reads, DeviceReads) else reads
+        check(lib().bc_pileup_summary_amplicons(self.h, C.byref(r), int(L), int(mbq), int(k), float(nf), float(nf2),
+                                                d_counts, d_cov, d_ent, d_sec, d_work, d_out, d_lo, d_hi,
+                                                int(n_tiles), d_amp))
 
     def amplicons(self, d_cov, d_ent, d_sec, L, d_lo, d_hi, n_tiles, d_out) -> None:
         check(lib().bc_amplicons(self.h, d_cov, d_ent, d_sec, int(L), d_lo, d_hi, int(n_tiles),

@@ -954,6 +954,23 @@ def _device_reference(ctx, reads, L, mbq, ncols, k, nf, nf2, mode, tiles, want_t
     outs = scratch.outputs(k, L, want_pc=(mode == "rows"))
     hist = scratch.get("hist", 4 * ncols * L)
     pc_ptr = outs["pc"].ptr if outs["pc"] else None
+    if reads.sorted and mode != "rows" and tiles:
+        # --summarise-with-bed: pileup, summary and every amplicon window in one library call (a
+        # deep batch's tail after kernel 1: kernel 2 + one launch)
+        work, dout = scratch.get("work", D.summary_work_bytes(L)), scratch.get("dout", 32)
+        lo = np.ascontiguousarray([a for a, _ in tiles], np.int64)
+        hi = np.ascontiguousarray([b for _, b in tiles], np.int64)
+        d_lo = scratch.get("amp_lo", lo.nbytes).upload(lo)
+        d_hi = scratch.get("amp_hi", hi.nbytes).upload(hi)
+        d_amp = scratch.get("amp", 48 * len(tiles))
+        ctx.pileup_summary_amplicons(reads, L, mbq, k, nf, nf2, hist.ptr, outs["cov"].ptr, outs["ent"].ptr,
+                                     outs["sec"].ptr, work.ptr, dout.ptr, d_lo.ptr, d_hi.ptr, len(tiles), d_amp.ptr)
+        bad = ctx.range_error()
+        s = dout.download(np.float64, 4)
+        amp = d_amp.download(np.float64, 6 * len(tiles)).reshape(-1, 6)
+        empty = [max(a, 0) > min(b, L - 1) for a, b in tiles]
+        return {"L": L, "avg_cov": np.float64(s[0]), "avg_ent": np.float64(s[1]), "nnz": int(s[2]),
+                "amplicons": (amp, empty)}, bad
     if reads.sorted and mode != "rows":
         # pileup + summary: the sparse sweep computes numpy's buffer partials in registers
         work, dout = scratch.get("work", D.summary_work_bytes(L)), scratch.get("dout", 32)

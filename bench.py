@@ -58,7 +58,7 @@ WORKLOADS = {  # BASELINE.json configs (per rank)
 }
 # the kernels named in the line (kernel_us, roofline.kernel): see DESIGN.md §3
 KERNEL_NAMES = {"pileup": "k_pileup", "solo": "k_pileup_solo", "rc": "k_rc", "stats": "k_stats_lane",
-                "amplicons": "k_amplicon", "summary": "k_sum_chunks + k_sum_final",
+                "amplicons": "k_amplicon (C4: k_tail, the summary fold and every window in one launch)", "summary": "k_sum_chunks + k_sum_final",
                 "solo_sum": "k_sum_reads + k_sum_exact + k_sum_buffers"}
 
 
@@ -419,6 +419,12 @@ class Workload:
         j = self._next()
         for side in self.ctxs[1:]:  # fork
             side.wait(main)
+        if self.d_tiles is not None:  # --summarise-with-bed (main.py:469-551): one library call
+            (_, L, _, reads, o), (d_lo, d_hi, d_amp) = self.work[0], self.d_tiles
+            main.pileup_summary_amplicons(reads[j], L, self.mbq, self.k, self.nf, self.nf2, o["counts"].ptr,
+                                          o["cov"].ptr, o["ent"].ptr, o["sec"].ptr, o["swork"].ptr, self.d_sum.ptr,
+                                          d_lo.ptr, d_hi.ptr, len(self.tiles), d_amp.ptr)
+            return
         for i, (_, L, _, reads, o) in enumerate(self.work):
             ctx = self.ctxs[self.on[i]]
             pc = o["pc"].ptr if o["pc"] is not None else None
@@ -441,10 +447,6 @@ class Workload:
         if self.summarise and self.fused_summary:  # every contig's fold, side by side
             ctx.summary_fold([w[1] for w in self.work], [w[4]["swork"].ptr for w in self.work],
                              [self.d_sum.ptr + 32 * i for i in range(len(self.work))])
-        if self.d_tiles is not None:  # the amplicon vectors (main.py:501-551) of the one contig
-            (_, L, _, _, o), (d_lo, d_hi, d_amp) = self.work[0], self.d_tiles
-            ctx.amplicons(o["cov"].ptr, o["ent"].ptr, o["sec"].ptr, L, d_lo.ptr, d_hi.ptr, len(self.tiles),
-                          d_amp.ptr)
 
     def pipelined(self, steps: int, sides: list):
         """K steps with 1 + len(sides) in flight: step i runs on context i mod n (the main one or

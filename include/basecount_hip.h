@@ -334,6 +334,18 @@ int bc_amplicons(bc_ctx* ctx, const int32_t* d_cov, const double* d_ent, const d
                  int64_t ref_len, const int64_t* d_lo, const int64_t* d_hi, int32_t n_tiles,
                  double* d_out);
 
+/* --summarise-with-bed for one reference (main.py:469-551): bc_pileup_summary and bc_amplicons
+ * in one call, same numbers bit for bit.  For a deep batch (the read-chunked k_rc) the tail after
+ * kernel 1 is two launches: kernel 2 that also leaves numpy's 128-position leaf partials in
+ * d_work, and ONE launch for the summary fold and every window's means and medians (instead of
+ * kernel 2, the summary's chunk sums, its fold and the amplicon kernel); other batches run
+ * bc_pileup_summary + bc_amplicons.  Arguments as those two (d_counts, d_cov, d_ent and d_sec all
+ * non-NULL: the windows read them; no percentages), n_tiles >= 0.                             */
+int bc_pileup_summary_amplicons(bc_ctx* ctx, const bc_reads* d_reads, int64_t ref_len, uint32_t min_base_quality,
+                                int k, double nf, double nf2, int32_t* d_counts, int32_t* d_cov, double* d_ent,
+                                double* d_sec, void* d_work, double* d_out, const int64_t* d_lo,
+                                const int64_t* d_hi, int32_t n_tiles, double* d_amp);
+
 /* ---- Multi-GPU: one process per GPU, RCCL over xGMI ---------------------------
  * Counting needs no exchange: references are independent, so each rank owns whole references
  * and runs the single-GPU path on them.  What crosses GPUs is small: the per-reference results

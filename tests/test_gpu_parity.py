@@ -843,6 +843,50 @@ def test_amplicons_match_numpy(ctx, wmax, ties):
         assert got[i].tolist() == [float(x) for x in e], (i, tiles[i])
 
 
+@pytest.mark.parametrize("L,n,mbq,k", [(8192 * 3 + 1711, 60_000, 0, 5), (8192 * 2, 40_000, 20, 6),
+                                        (5_000, 30_000, 0, 5), (40_003, 50_000, 0, 6)])
+def test_pileup_summary_amplicons_fused_tail(ctx, L, n, mbq, k):
+    """bc_pileup_summary_amplicons on the read-chunked path (kernel 1, kernel 2 with numpy's leaf
+    partials, then ONE launch for the summary fold and every window): the summary's four numbers
+    equal numpy over the oracle's coverage / entropies (main.py:469-499), every window's means and
+    medians the oracle's (main.py:519-551) -- amplicon-sized windows (rank-counted medians), wide
+    ones (radix select), empty and clipped ones -- and bc_pileup_summary (no windows, summary only
+    too) gives the same summary."""
+    rng = np.random.default_rng(L + n)
+    b = random_batch(rng, L, n)
+    exp, (br, _) = O.bcount(L, mbq, b)
+    assert br == -1
+    ocov, _, oent, osec = O.stats(exp, k == 6)
+    want = [np.mean(ocov.astype(np.int64)), np.mean(oent), float(np.count_nonzero(ocov)), float(ocov.astype(np.int64).sum())]
+    tiles = [(int(a), int(a + w)) for a, w in zip(rng.integers(-20, L, 60), rng.integers(-3, 420, 60))]
+    tiles += [(0, 0), (L - 1, L + 10), (5, 4), (100, 100 + 1_500), (0, L - 1)]
+    lo = np.array([t[0] for t in tiles], np.int64)
+    hi = np.array([t[1] for t in tiles], np.int64)
+    ctx.set_shape("rc")
+    try:
+        nf, nf2 = norm_factors(k)
+        r = D.DeviceReads(ctx, b)
+        counts, cov, ent, sec = ctx.alloc(4 * k * L), ctx.alloc(4 * L), ctx.alloc(8 * L), ctx.alloc(8 * L)
+        work, dout = ctx.alloc(D.summary_work_bytes(L)), ctx.alloc(32)
+        dlo, dhi, damp = ctx.alloc(lo.nbytes).upload(lo), ctx.alloc(hi.nbytes).upload(hi), ctx.alloc(48 * len(tiles))
+        for _ in range(2):  # (the second call on the scratch the first left zeroed)
+            ctx.pileup_summary_amplicons(r, L, mbq, k, nf, nf2, counts.ptr, cov.ptr, ent.ptr, sec.ptr, work.ptr,
+                                         dout.ptr, dlo.ptr, dhi.ptr, len(tiles), damp.ptr)
+            assert ctx.range_error() == -1
+            assert dout.download(np.float64, 4).tolist() == want
+            got = damp.download(np.float64, 6 * len(tiles)).reshape(-1, 6)
+            for i, e in enumerate(O.amplicons(ocov, oent, osec, tiles)):
+                assert got[i].tolist() == [float(x) for x in e], (i, tiles[i])
+        assert np.array_equal(counts.download(np.int32, k * L).reshape(k, L), exp[:, :k].T.astype(np.int32))
+        for outs in ((counts.ptr, cov.ptr, ent.ptr, sec.ptr), (None, None, None, None)):
+            dout.zero()
+            ctx.pileup_summary(r, L, mbq, k, nf, nf2, outs[0], outs[1], None, outs[2], outs[3], work.ptr, dout.ptr)
+            assert dout.download(np.float64, 4).tolist() == want
+        r.free()
+    finally:
+        ctx.set_shape("auto")
+
+
 # ------------------------------------------------------------------ CLI vs reference goldens
 def _run_cli(argv):
     from basecount_amd.main import run

@@ -137,8 +137,45 @@ def make_reads(contigs, reads_per_contig: int, mixed: bool, seed: int, read_len:
 
 def make_config(name: str, unsorted: bool = False, contigs=None, reads=None) -> ReadSet:
     c = CONFIGS[name.lower()]
+    if c.get("per_contig"):  # each contig's reads from its own seed (contig_reads)
+        cs = list(contigs or c["contigs"])
+        return contig_reads(cs, range(len(cs)), reads or c["reads"], c["mixed"], c["seed"], unsorted=unsorted)
     return make_reads(contigs or c["contigs"], reads or c["reads"], c["mixed"], c["seed"],
                       unsorted=unsorted)
+
+
+def contig_reads(contigs, indices, reads_per_contig: int, mixed: bool, seed: int, unsorted: bool = False) -> ReadSet:
+    """The reads of contigs[i] for i in `indices`, each contig from its own seed (seed + 1000003 i),
+    so a contig's reads do not depend on which others are generated with it: a rank holding a
+    shard of the contigs (bench.py, several GPUs) counts exactly the reads one process would."""
+    parts = [make_reads([contigs[i]], reads_per_contig, mixed, seed + 1000003 * i, unsorted=unsorted)
+             for i in indices]
+    return concat(parts, [contigs[i][0] for i in indices], [int(contigs[i][1]) for i in indices])
+
+
+def concat(parts, references, lengths) -> ReadSet:
+    """One ReadSet of several (part k's reads on contig k)."""
+    if not parts:
+        z = lambda dt: np.zeros(0, dt)  # noqa: E731
+        return ReadSet(references=[], lengths=[], tid=z(np.int32), pos=z(np.int32), flag=z(np.uint16),
+                       mapq=z(np.uint8), cig_off=np.zeros(1, np.uint64), cigar=z(np.uint32), l_seq=z(np.int32),
+                       seq_off=np.zeros(1, np.uint64), seq=z(np.uint8), qual_off=np.zeros(1, np.uint64),
+                       qual=z(np.uint8), qstart=z(np.int32))
+    tid = np.concatenate([np.full(p.n, k, np.int32) for k, p in enumerate(parts)])
+
+    def offs(name):
+        out, base = [np.zeros(1, np.uint64)], np.uint64(0)
+        for p in parts:
+            o = getattr(p, name)
+            out.append(o[1:] + base)
+            base += o[-1]
+        return np.concatenate(out).astype(np.uint64)
+
+    cat = lambda name: np.concatenate([getattr(p, name) for p in parts])  # noqa: E731
+    return ReadSet(references=list(references), lengths=list(lengths), tid=tid, pos=cat("pos"), flag=cat("flag"),
+                   mapq=cat("mapq"), cig_off=offs("cig_off"), cigar=cat("cigar"), l_seq=cat("l_seq"),
+                   seq_off=offs("seq_off"), seq=cat("seq"), qual_off=offs("qual_off"), qual=cat("qual"),
+                   qstart=cat("qstart"))
 
 
 def subset(rs: ReadSet, order) -> ReadSet:

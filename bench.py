@@ -308,7 +308,6 @@ class Workload:
         from basecount_amd import device as D
         from basecount_amd import synth
         from basecount_amd.bam import seq_to_event
-        from basecount_amd.dist import shard
         from basecount_amd.main import norm_factors
 
         self.D, self.ctx, self.cfg, self.mbq = D, ctx, cfg, mbq
@@ -317,9 +316,10 @@ class Workload:
         self.mixed = c["mixed"]
         if self.per_contig:
             contigs = list(c["contigs"])
-            owner = shard([n for n, _ in contigs], dict(contigs), world)
-            mine = [(n, L) for n, L in contigs if owner[n] == rank]
-            self.rs = synth.make_reads(mine, c["reads"], c["mixed"], c["seed"] + 1000 * rank)
+            _, mine = contig_plan(contigs, world, rank)
+            # each contig's reads from its own seed: the ranks together count exactly the reads
+            # one process would (strong scaling over the same job)
+            self.rs = synth.contig_reads(contigs, mine, c["reads"], c["mixed"], c["seed"])
             self.total_positions = sum(L for _, L in contigs)
         else:
             name = "MN908947.3" if world == 1 else f"contig{rank}"
@@ -574,6 +574,15 @@ class Workload:
             x.free()
         self.d_tiles = None
         self.work = []
+
+
+def contig_plan(contigs, world: int, rank: int):
+    """C5's sharding: contigs to ranks by LPT on their length (dist.shard); returns
+    (owner by name, this rank's contig indices in config order)."""
+    from basecount_amd.dist import shard
+
+    owner = shard([n for n, _ in contigs], dict(contigs), world)
+    return owner, [i for i, (n, _) in enumerate(contigs) if owner[n] == rank]
 
 
 def strip_index(r) -> None:

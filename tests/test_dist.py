@@ -217,3 +217,32 @@ def test_comm_init_is_agreed_by_every_rank(tmp_path, fail_rank, fail_what):
         up = fail_what == "init" and r != fail_rank
         assert d == (f"[{1000 + r}]" if up else "[]"), (r, d)
 
+
+def test_bench_c5_sharding_world4(tmp_path):
+    """bench.py's N > 1 C5 leg rehearsed on 4 gloo ranks (the counting by the
+    oracle, contigs scaled down 4000x): the LPT plan keeps every rank's positions within one
+    chr1 of the mean (at GRCh38 lengths too), and the per-contig summaries gathered to rank 0
+    equal one process computing every contig (a contig's reads do not depend on its rank)."""
+    import json
+
+    from basecount_amd import synth
+
+    out = tmp_path / "c5.json"
+    world = 4
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+               BASECOUNT_DIST_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               BASECOUNT_RDZV_PORT=str(_free_port()))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "bench_c5_worker.py"), str(out)],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stderr=subprocess.PIPE)
+             for r in range(world)]
+    errs = [p.communicate(timeout=240)[1] for p in procs]
+    assert [p.returncode for p in procs] == [0] * world, [e.decode()[-2000:] for e in errs]
+    res = json.loads(out.read_text())
+    assert res["got"] == res["want"]
+    assert sorted(set(res["owner"].values())) == list(range(world))
+    for loads, contigs in ((res["loads"], [(n, L // 4000) for n, L in synth.GRCH38]), (res["full_loads"], synth.GRCH38)):
+        longest = max(L for _, L in contigs)
+        assert sum(loads) == sum(L for _, L in contigs)
+        assert max(loads) - min(loads) <= longest  # LPT: within one chr1
+        assert max(loads) <= sum(loads) / world + longest
+

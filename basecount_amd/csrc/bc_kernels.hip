@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 // in LDS and each element's rank is counted against all of them (ties by index: the sorted
 // order's position, exact), so the elements of rank (n-1)/2 and n/2 are the middle ones; longer
 // windows take the radix select.  Same values as k_amplicon + k_sum_chunks + k_sum_final.
-constexpr int kTailWin = 512;
+constexpr int kTailWin = 512;  // two positions per thread of a 256-thread block
 __global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* ent, const double* sec, int64_t L,
                                               const int64_t* lo_a, const int64_t* hi_a, int n_tiles, double* amp,
                                               Leaves lv, double* out) {
@@ -1225,11 +1225,21 @@ __global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* 
         if (m > 0) {
             extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
             double* s_ent = (double*)dyn;
-            for (int i = t; i < m; i += 256) {
-                const int32_t c = cov[lv.full + i];
-                s_ent[i] = ent[lv.full + i];
-                cs += c;
-                nz += c != 0;
+            // every load of the buffer issued before any is used (one round trip, not m / 256)
+            int cv[kNpBuf / 256];
+            double ev[kNpBuf / 256];
+#pragma unroll
+            for (int j = 0; j < kNpBuf / 256; ++j) {
+                const int i = t + 256 * j;
+                cv[j] = i < m ? cov[lv.full + i] : 0;
+                ev[j] = i < m ? ent[lv.full + i] : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < kNpBuf / 256; ++j) {
+                const int i = t + 256 * j;
+                cs += cv[j];
+                nz += cv[j] != 0;
+                if (i < m) s_ent[i] = ev[j];
             }
             __syncthreads();
             const double e = pw_block(s_ent, m, s_off, s_len, s_val);
@@ -1266,24 +1276,28 @@ __global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* 
     unsigned long long a, b;
     double mean;
     if (n <= kTailWin) {  // (uniform)
-        for (int i = t; i < n; i += 256) s_key[i] = key(i);
-        __syncthreads();
-        // ranks of elements t and t + 256: #smaller + #equal before it
         const int i0 = t, i1 = t + 256;
-        const unsigned long long x0 = i0 < n ? s_key[i0] : 0ull, x1 = i1 < n ? s_key[i1] : 0ull;
-        int r0 = 0, r1 = 0;
+        const unsigned long long x0 = i0 < n ? key(i0) : 0ull, x1 = i1 < n ? key(i1) : 0ull;  // (both in flight)
+        if (i0 < n) s_key[i0] = x0;
+        if (i1 < n) s_key[i1] = x1;
+        __syncthreads();
+        // elements t and t + 256: how many keys are smaller, how many equal; the sorted order
+        // holds x at positions [lt, lt + eq), so x is the k-th smallest iff lt <= k < lt + eq
+        // (equal keys write the same value)
+        int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0;
         for (int j = 0; j < n; ++j) {
             const unsigned long long y = s_key[j];  // (one address per wave: a broadcast)
-            r0 += (y < x0 || (y == x0 && j < i0)) ? 1 : 0;
-            r1 += (y < x1 || (y == x1 && j < i1)) ? 1 : 0;
+            lt0 += y < x0 ? 1 : 0;
+            eq0 += y == x0 ? 1 : 0;
+            lt1 += y < x1 ? 1 : 0;
+            eq1 += y == x1 ? 1 : 0;
         }
-        if (i0 < n && r0 == k1) s_sel[0] = x0;
-        if (i0 < n && r0 == k2) s_sel[1] = x0;
-        if (i1 < n && r1 == k1) s_sel[0] = x1;
-        if (i1 < n && r1 == k2) s_sel[1] = x1;
+        if (i0 < n && lt0 <= k1 && k1 < lt0 + eq0) s_sel[0] = x0;
+        if (i0 < n && lt0 <= k2 && k2 < lt0 + eq0) s_sel[1] = x0;
+        if (i1 < n && lt1 <= k1 && k1 < lt1 + eq1) s_sel[0] = x1;
+        if (i1 < n && lt1 <= k2 && k2 < lt1 + eq1) s_sel[1] = x1;
         if (q == 0) {  // (uniform) the exact integer sum
-            long long cs = 0;
-            for (int i = t; i < n; i += 256) cs += (long long)s_key[i];
+            long long cs = (i0 < n ? (long long)x0 : 0) + (i1 < n ? (long long)x1 : 0);
             cs = block_sum_i64(cs, s_red);  // (contains the barriers after the rank writes)
             mean = (double)cs / (double)n;
         } else {  // numpy's pairwise mean over the window (values in LDS, as doubles)

@@ -1180,26 +1180,29 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 // every whole buffer's 64 leaves (k_stats_lane<LEAVES>) added up numpy's tree by a wave, the
 // buffers folded in order, the last partial buffer's pairwise sum from LDS (pw_block), the exact
 // coverage sum and non-zero count.  The windows' medians: a window of <= 512 positions is staged
-// in LDS and each element's rank is counted against all of them (ties by index: the sorted
-// order's position, exact), so the elements of rank (n-1)/2 and n/2 are the middle ones; longer
-// windows take the radix select.  Same values as k_amplicon + k_sum_chunks + k_sum_final.
-constexpr int kTailWin = 512;  // two positions per thread of a 256-thread block
-__global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* ent, const double* sec, int64_t L,
+// in LDS, one element per thread, and each thread counts the keys smaller than its own: the
+// k-th smallest value is the largest one with at most k smaller keys (an LDS atomic max), so the
+// middle elements need one compare per key pair and no sort; longer windows take the radix
+// select.  Same values as k_amplicon + k_sum_chunks + k_sum_final.
+constexpr int kTailThreads = 512;
+constexpr int kTailWin = kTailThreads;  // one position per thread
+__global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const double* ent, const double* sec, int64_t L,
                                               const int64_t* lo_a, const int64_t* hi_a, int n_tiles, double* amp,
                                               Leaves lv, double* out) {
     __shared__ unsigned s_hist[256];
     __shared__ unsigned long long s_sel[2];
-    __shared__ long long s_red[8];
+    __shared__ long long s_red[kTailThreads / 64];
     __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
     __shared__ double s_val[2 << kLv];
     __shared__ unsigned long long s_key[kTailWin];
-    __shared__ double s_buf[4];
+    constexpr int NW = kTailThreads / 64;
+    __shared__ double s_buf[NW];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if ((int)blockIdx.x == 3 * n_tiles) {  // (uniform) the summary
         const int64_t nfull = lv.full / kNpBuf;
         double s = 0.0;
         long long cs = 0, nz = 0;
-        for (int64_t b0 = 0; b0 < nfull; b0 += 4) {
+        for (int64_t b0 = 0; b0 < nfull; b0 += NW) {
             const int64_t b = b0 + wave;
             double v = 0.0;
             if (b < nfull) {
@@ -1218,7 +1221,7 @@ __global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* 
             if (lane == 0) s_buf[wave] = v;
             __syncthreads();
             if (t == 0)
-                for (int w = 0; w < 4 && b0 + w < nfull; ++w) s += s_buf[w];  // buffers in order
+                for (int w = 0; w < NW && b0 + w < nfull; ++w) s += s_buf[w];  // buffers in order
             __syncthreads();
         }
         const int m = (int)(L - lv.full);  // the last, partial buffer: [full, L)
@@ -1226,17 +1229,17 @@ __global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* 
             extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
             double* s_ent = (double*)dyn;
             // every load of the buffer issued before any is used (one round trip, not m / 256)
-            int cv[kNpBuf / 256];
-            double ev[kNpBuf / 256];
+            int cv[kNpBuf / kTailThreads];
+            double ev[kNpBuf / kTailThreads];
 #pragma unroll
-            for (int j = 0; j < kNpBuf / 256; ++j) {
-                const int i = t + 256 * j;
+            for (int j = 0; j < kNpBuf / kTailThreads; ++j) {
+                const int i = t + kTailThreads * j;
                 cv[j] = i < m ? cov[lv.full + i] : 0;
                 ev[j] = i < m ? ent[lv.full + i] : 0.0;
             }
 #pragma unroll
-            for (int j = 0; j < kNpBuf / 256; ++j) {
-                const int i = t + 256 * j;
+            for (int j = 0; j < kNpBuf / kTailThreads; ++j) {
+                const int i = t + kTailThreads * j;
                 cs += cv[j];
                 nz += cv[j] != 0;
                 if (i < m) s_ent[i] = ev[j];
@@ -1276,28 +1279,19 @@ __global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* 
     unsigned long long a, b;
     double mean;
     if (n <= kTailWin) {  // (uniform)
-        const int i0 = t, i1 = t + 256;
-        const unsigned long long x0 = i0 < n ? key(i0) : 0ull, x1 = i1 < n ? key(i1) : 0ull;  // (both in flight)
-        if (i0 < n) s_key[i0] = x0;
-        if (i1 < n) s_key[i1] = x1;
+        const bool in = t < n;
+        const unsigned long long x = in ? key(t) : 0ull;
+        if (in) s_key[t] = x;
+        if (t < 2) s_sel[t] = 0ull;
         __syncthreads();
-        // elements t and t + 256: how many keys are smaller, how many equal; the sorted order
-        // holds x at positions [lt, lt + eq), so x is the k-th smallest iff lt <= k < lt + eq
-        // (equal keys write the same value)
-        int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0;
-        for (int j = 0; j < n; ++j) {
-            const unsigned long long y = s_key[j];  // (one address per wave: a broadcast)
-            lt0 += y < x0 ? 1 : 0;
-            eq0 += y == x0 ? 1 : 0;
-            lt1 += y < x1 ? 1 : 0;
-            eq1 += y == x1 ? 1 : 0;
-        }
-        if (i0 < n && lt0 <= k1 && k1 < lt0 + eq0) s_sel[0] = x0;
-        if (i0 < n && lt0 <= k2 && k2 < lt0 + eq0) s_sel[1] = x0;
-        if (i1 < n && lt1 <= k1 && k1 < lt1 + eq1) s_sel[0] = x1;
-        if (i1 < n && lt1 <= k2 && k2 < lt1 + eq1) s_sel[1] = x1;
+        // the keys smaller than x: x <= (k-th smallest) iff at most k keys are smaller, so the
+        // k-th smallest is the largest such x
+        int lt = 0;
+        for (int j = 0; j < n; ++j) lt += s_key[j] < x ? 1 : 0;  // (one address per wave: a broadcast)
+        if (in && lt <= k1) atomicMax(&s_sel[0], x);
+        if (in && lt <= k2) atomicMax(&s_sel[1], x);
         if (q == 0) {  // (uniform) the exact integer sum
-            long long cs = (i0 < n ? (long long)x0 : 0) + (i1 < n ? (long long)x1 : 0);
+            long long cs = in ? (long long)x : 0;
             cs = block_sum_i64(cs, s_red);  // (contains the barriers after the rank writes)
             mean = (double)cs / (double)n;
         } else {  // numpy's pairwise mean over the window (values in LDS, as doubles)
@@ -1312,7 +1306,7 @@ __global__ __launch_bounds__(256) void k_tail(const int32_t* cov, const double* 
         b = k2 != k1 ? radix_select(key, n, k2, bits, s_hist, s_sel) : a;
         if (q == 0) {
             long long cs = 0;
-            for (int64_t i = t; i < n; i += 256) cs += (long long)(uint32_t)cov[lo + i];
+            for (int64_t i = t; i < n; i += kTailThreads) cs += (long long)(uint32_t)cov[lo + i];
             cs = block_sum_i64(cs, s_red);
             mean = (double)cs / (double)n;
         } else {
@@ -1463,7 +1457,7 @@ hipError_t launch_tail(hipStream_t s, const int32_t* cov, const double* ent, con
     if (L <= 0) return hipSuccess;
     const Leaves lv = summary_leaves(work, L);
     const size_t tail_lds = (size_t)(L - lv.full) * sizeof(double);
-    hipLaunchKernelGGL(k_tail, dim3((unsigned)(3 * n_tiles + 1)), dim3(256), tail_lds, s, cov, ent, sec, L, lo, hi,
+    hipLaunchKernelGGL(k_tail, dim3((unsigned)(3 * n_tiles + 1)), dim3(kTailThreads), tail_lds, s, cov, ent, sec, L, lo, hi,
                        n_tiles, amp, lv, out);
     return hipGetLastError();
 }

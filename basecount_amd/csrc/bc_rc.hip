@@ -322,9 +322,6 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
     // image path, which overwrites both, uses neither (1 KiB of LDS kept for the gather stage:
     // a 512-byte larger block no longer fits three times into a CU, k_rc 46 -> 71 us at C3)
     int32_t* const rpos = (int32_t*)(rec + kRecU4);
-    // gather staging's per-read table (first word, words to move), past the read positions
-    uint32_t* const gtab = (uint32_t*)(rec + kRecAll);
-    static_assert(kRecAll * 16 + 8 * kRcReads <= (int)sizeof(rec), "the gather table fits the records region");
     // (the gather stage's slots reach kGStage bytes; both layouts keep kPadW words of pad after)
     __shared__ __attribute__((aligned(16))) uint8_t stage_raw[(kStage > kGStage ? kStage : kGStage) + 8 * kPadW];  // + pads
     __shared__ uint32_t hist[3][kRcWinPos];                              // {A|C, G|T, DS|N}
@@ -418,6 +415,26 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const uint32_t buf_end = (uint32_t)(A.seq_words * 4 < 0xFFFFFFFFll ? A.seq_words * 4 : 0xFFFFFFFFll);
         spec_hi = spec_hi < buf_end ? spec_hi : buf_end;
         const bool spec = !QUAL && spec_hi > spec_lo && spec_hi - spec_lo <= (uint32_t)kStage && !(BC_ABL(A) & 512);
+        // Gather staging (see kRcSlot): each read's slot words by LDS-DMA in stage order.  A wave's
+        // 20 instructions cover exactly its own 64 reads' slots, so lane l of instruction e moves
+        // word k of read r = (64 e + l) / 20 of the wave, whose first word and word count come
+        // from read r's lane (a shuffle: no table, no barrier).  nwords(): this lane's read's words.
+        auto gather_dma = [&](uint32_t src_word, uint32_t nwords) {
+#pragma unroll 1
+            for (int e = 0; e < kRcSlot / 4; ++e) {
+                const uint32_t g = (uint32_t)(e * 64 + lane);
+                const int r = (int)((g * 3277u) >> 16);  // g / 20 (g < 1280)
+                const uint32_t k = g - (uint32_t)(kRcSlot / 4) * (uint32_t)r;
+                const uint32_t src = (uint32_t)__shfl((int)src_word, r), nw = (uint32_t)__shfl((int)nwords, r);
+                if (k < nw)
+                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(A.seq + src + 4u * k),
+                                                     (lds_void_t*)(stage + 256 * (wave * (kRcSlot / 4) + e)), 4, 0, 0);
+            }
+        };
+        // a chunk whose reads' sequences are not one short segment (a batch sorted on the device
+        // without moving its sequence) is gathered speculatively, now, in parallel with the decode
+        // and the bounds: every read's whole slot (the words the buffer holds), checked after
+        const bool spec_g = kGather && !QUAL && !spec && !(BC_ABL(A) & 512);  // (uniform)
         // The loads prefetched during the previous chunk (fields, run records or CIGAR words) are
         // waited for HERE, before the stage DMA is queued behind them: vmcnt is in order and the
         // compiler cannot count the DMA passes, so a wait at their first use below would be a
@@ -425,6 +442,11 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         // the copy's round trip).  They were issued a whole phase ago: this wait is ~free.
         if (kEarlyWait) __builtin_amdgcn_s_waitcnt(kWaitVm0);
         if (spec) stage_dma<kRcThreads>(stage, A.seq + spec_lo, spec_hi - spec_lo, tid);
+        if (spec_g) {
+            const uint32_t w0 = (msn >> 1) & ~3u;
+            const uint32_t left = buf_end > w0 ? (buf_end - w0) >> 2 : 0u;  // words of the buffer from w0
+            gather_dma(w0, valid ? (left < (uint32_t)(kRcSlot / 4) ? left : (uint32_t)(kRcSlot / 4)) : 0u);
+        }
         RunTable T;
         T.nrun = 0;
         T.gap = T.complex = false;
@@ -527,11 +549,6 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
             v[5] = simple ? run_shape(T) : 0u;
             v[6] = (simple && T.gap) ? 1u : 0u;
             v[7] = simple ? rbytes : 0u;
-            // gather staging's table, in case the chunk takes it (read before this chunk's records
-            // or image are written, past the records and read positions): the read's first word
-            // and the words to move (0: not gathered)
-            gtab[tid] = (msn >> 1) & ~3u;
-            gtab[kRcReads + tid] = (simple && !over_slot) ? (((msn >> 1) & 3u) + rbytes + 3u) >> 2 : 0u;
             RC_STAMP(1);
             block_reduce<8, kRcWaves>(v, is_max, red);  // contains a __syncthreads
             RC_STAMP(2);
@@ -573,7 +590,7 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
         const bool img_path = inlds && img_shape;
         const int gpad = NWc;  // (uniform) the image's group padding (see rec)
         uint32_t* const mycol = img + tid * kImgRows + (tid >> 5) * gpad;  // this read's image column
-        if (spec && !spec_ok) {  // (uniform) the speculative copy is overwritten
+        if ((spec && !spec_ok) || (spec_g && !gather)) {  // (uniform) the speculative copy is overwritten
             stage_wait();
             __syncthreads();
         }
@@ -606,17 +623,8 @@ __global__ __launch_bounds__(NT, 3) void k_rc(RcArgs A) {
                 *(uint4*)(stage + off) = q4;
             }
         }
-        if (gather) {  // (uniform) the slots' words in stage order, a few reads per instruction
-            // (not unrolled: the 40 table reads of an unrolled loop, hoisted together, spill)
-#pragma unroll 1
-            for (int e = 0; e < kRcSlot / 4; ++e) {
-                const uint32_t g = (uint32_t)((wave * (kRcSlot / 4) + e) * 64 + lane);  // stage word
-                const uint32_t r = (g * 3277u) >> 16, k = g - (uint32_t)(kRcSlot / 4) * r;  // slot r, word k
-                if (k < gtab[kRcReads + r])
-                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(A.seq + gtab[r] + 4u * k),
-                                                     (lds_void_t*)(stage + 256 * (wave * (kRcSlot / 4) + e)), 4, 0, 0);
-            }
-        }
+        if (gather && !spec_g)  // (uniform) not gathered at the chunk start: the exact words now
+            gather_dma((msn >> 1) & ~3u, (simple && !over_slot) ? (((msn >> 1) & 3u) + rbytes + 3u) >> 2 : 0u);
         // ---- records (pos kept for complex / padding entries so pos[] stays sorted)
         {
             uint32_t rr[kMaxRuns], nb[kMaxRuns];

@@ -1286,8 +1286,15 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
         __syncthreads();
         // the keys smaller than x: x <= (k-th smallest) iff at most k keys are smaller, so the
         // k-th smallest is the largest such x
+        // (broadcast reads, 16 issued before they are compared: one LDS round trip per 16 keys)
         int lt = 0;
-        for (int j = 0; j < n; ++j) lt += s_key[j] < x ? 1 : 0;  // (one address per wave: a broadcast)
+        for (int j0 = 0; j0 < n; j0 += 16) {
+            unsigned long long y[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) y[u] = j0 + u < n ? s_key[j0 + u] : ~0ull;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) lt += y[u] < x ? 1 : 0;
+        }
         if (in && lt <= k1) atomicMax(&s_sel[0], x);
         if (in && lt <= k2) atomicMax(&s_sel[1], x);
         if (q == 0) {  // (uniform) the exact integer sum

@@ -447,6 +447,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(SortArgs A) {
 template <bool FIELDS>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     __shared__ uint32_t next[kBktMax], pre[kBktMax];
+    __shared__ __attribute__((aligned(16))) uint32_t dscr[(FIELDS && kSortRuns) ? 8 * kBktThreads : 4];
     __shared__ uint32_t ws[kBktThreads / 64];
     __shared__ uint32_t rq, rf;
     const int H = A.nbkt, nb = A.nblk, b = blockIdx.x;
@@ -537,10 +538,15 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
                     (int)wave_reduce<true>(i0 + (int64_t)u * kBktThreads < end ? (cn[u] < (uint32_t)kPre ? cn[u] : (uint32_t)kPre) : 0u));
 #pragma unroll
             for (int u = 0; u < B; ++u) {
-                const int64_t i = i0 + (int64_t)u * kBktThreads;
-                if (i >= end) break;
+                const bool in = i0 + (int64_t)u * kBktThreads < end;
+                // decode_fast2 (k_rc's own image decode, ~12 VALU per op; the lane's 8 scratch
+                // words in LDS), decode_runs for a wave with a read it declines
+                RunTable T;
+                const bool ok = in ? decode_fast2(w[u], cn[u], cm[u], dscr + 8 * threadIdx.x, T) : true;
+                if (__ballot(!ok) && in) T = decode_runs<2>(w[u], cn[u], cm[u]);
+                if (!in) continue;
                 uint32_t rr[4];
-                pack_runs(decode_runs<2>(w[u], cn[u], cm[u]), rr);
+                pack_runs(T, rr);
                 const uint32_t j = atomicAdd(&next[p[u] >> A.wbits], 1u);
                 A.brec[j] = make_uint4(p[u], cb[u], sn[u], cn[u]);
                 A.brun[j] = make_uint4(rr[0], rr[1], rr[2], rr[3]);

@@ -607,6 +607,92 @@ __device__ double pw_block(const double* a, int m, int* s_off, int* s_len, doubl
     return r;
 }
 
+// The same sum, pw_block's tree, without its 14 barriers and one-thread leaves: every leaf slot
+// (kLv levels of numpy's split: a leaf passes itself down as the left child, an empty right one)
+// is found by descending its bit path, its eight strided accumulators are eight threads'
+// (every load issued together, unguarded: clamped, and the extra ones selected to -0.0, which
+// adds exactly nothing to any double), combined by shuffles in numpy's order; then one wave adds
+// the slots up the tree: node i of level d sits in lane i << (6 - d), its right child 2^(5-d)
+// lanes up (a shuffle down), and each lane's descent recorded which of its ancestors split.
+// a: m <= 8192 doubles (LDS or global); s_leaf: 2^kLv doubles of LDS; NT threads (all call).
+// Returns the value in thread 0 only.
+__device__ __forceinline__ void pw_node(int m, int level, int idx, int& off, int& len) {
+    // node idx of the given level (level 0: the root) of numpy's recursion over m elements
+    // (branch-free: an unsplit node is its own left child, n2 = len, and an empty right one)
+    off = 0;
+    len = m;
+    for (int l = 0; l < level; ++l) {
+        const int bit = (idx >> (level - 1 - l)) & 1;
+        const int n2 = len > 128 ? (len >> 1) & ~7 : len;  // numpy: n/2 less its remainder mod 8
+        off += bit ? n2 : 0;
+        len = bit ? len - n2 : n2;
+    }
+}
+template <int NT>
+__device__ __forceinline__ double pw_fast(const double* a, int m, double* s_leaf) {
+    constexpr int kSlots = 1 << kLv, R = 8 * kSlots / NT;
+    static_assert(R * NT == 8 * kSlots, "NT must divide 8 x 2^kLv");
+    const int t = threadIdx.x, j = t & 7;  // (NT is a multiple of 8: every task of a thread has accumulator j)
+    int len[R], full[R];
+    double v[R][16], rem[R][7];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {  // every task's loads issued first
+        int off;
+        pw_node(m, kLv, (t + NT * q) >> 3, off, len[q]);
+        full[q] = len[q] & ~7;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = j + 8 * u;
+            v[q][u] = a[off + (i < full[q] ? i : 0)];
+        }
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {  // the leaf's last len % 8 (or, below 8, all) elements
+            const int i = full[q] + u;
+            rem[q][u] = a[off + (i < len[q] ? i : 0)];
+        }
+    }
+    double r[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        double x = v[q][0];
+#pragma unroll
+        for (int u = 1; u < 16; ++u) x = x + (j + 8 * u < full[q] ? v[q][u] : -0.0);
+        x = x + __shfl_down(x, 1);  // (r0+r1), (r2+r3), ...
+        x = x + __shfl_down(x, 2);
+        x = x + __shfl_down(x, 4);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+        if (len[q] < 8) x = 0.0;    // numpy: n < 8 sums from 0, in order
+#pragma unroll
+        for (int u = 0; u < 7; ++u) x = x + (full[q] + u < len[q] ? rem[q][u] : -0.0);
+        r[q] = x;
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+        if (((t + NT * q) & 7) == 0) s_leaf[(t + NT * q) >> 3] = r[q];
+    __syncthreads();
+    double res = 0.0;
+    if (t < 64) {
+        // lane t's descent to node t of level kLv - 1, recording which ancestors split
+        int n = m;
+        unsigned split = 0;
+#pragma unroll
+        for (int l = 0; l < kLv - 1; ++l) {
+            split |= (unsigned)(n > 128) << l;
+            const int n2 = n > 128 ? (n >> 1) & ~7 : n;
+            n = ((t >> (kLv - 2 - l)) & 1) ? n - n2 : n2;
+        }
+        const double v0 = s_leaf[2 * t], v1 = s_leaf[2 * t + 1];
+        double val = n > 128 ? v0 + v1 : v0;
+#pragma unroll
+        for (int d = kLv - 2; d >= 0; --d) {
+            const double c1 = __shfl_down(val, 1 << (kLv - 2 - d));
+            val = ((split >> d) & 1) ? val + c1 : val;
+        }
+        res = val;
+    }
+    __syncthreads();  // s_leaf reusable
+    return res;
+}
+
 // Full 8192-element buffer with the fixed tree: 64 leaves of 128; 256 threads, thread t owns
 // accumulators {2(t&3), 2(t&3)+1} of leaf t>>2.  Value valid in thread 0.
 template <class F>
@@ -1184,6 +1270,12 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 // k-th smallest value is the largest one with at most k smaller keys (an LDS atomic max), so the
 // middle elements need one compare per key pair and no sort; longer windows take the radix
 // select.  Same values as k_amplicon + k_sum_chunks + k_sum_final.
+#ifdef BC_TAIL_TRACE  // diagnostic: block 0's phase stamps (s_memtime) after the windows' outputs
+#define TAIL_STAMP(k) \
+    do { if (blockIdx.x == 0 && threadIdx.x == 0) amp[6 * n_tiles + (k)] = (double)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define TAIL_STAMP(k) do {} while (0)
+#endif
 constexpr int kTailThreads = 512;
 constexpr int kTailWin = kTailThreads;  // one position per thread
 __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const double* ent, const double* sec, int64_t L,
@@ -1194,11 +1286,13 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
     __shared__ long long s_red[kTailThreads / 64];
     __shared__ int s_off[(2 << kLv) - 1], s_len[(2 << kLv) - 1];
     __shared__ double s_val[2 << kLv];
-    __shared__ unsigned long long s_key[kTailWin];
+    __shared__ unsigned long long s_key[kTailWin];  // the window's values in order (numpy's mean)
+    __shared__ unsigned long long s_run[kTailWin];  // ... and each wave's 64 of them sorted
     constexpr int NW = kTailThreads / 64;
     __shared__ double s_buf[NW];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if ((int)blockIdx.x == 3 * n_tiles) {  // (uniform) the summary
+        TAIL_STAMP(0);
         const int64_t nfull = lv.full / kNpBuf;
         double s = 0.0;
         long long cs = 0, nz = 0;
@@ -1224,29 +1318,26 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
                 for (int w = 0; w < NW && b0 + w < nfull; ++w) s += s_buf[w];  // buffers in order
             __syncthreads();
         }
+        TAIL_STAMP(1);
         const int m = (int)(L - lv.full);  // the last, partial buffer: [full, L)
         if (m > 0) {
-            extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-            double* s_ent = (double*)dyn;
-            // every load of the buffer issued before any is used (one round trip, not m / 256)
+            // its coverage loads issued first, then its pairwise sum straight from the array
             int cv[kNpBuf / kTailThreads];
-            double ev[kNpBuf / kTailThreads];
 #pragma unroll
             for (int j = 0; j < kNpBuf / kTailThreads; ++j) {
                 const int i = t + kTailThreads * j;
-                cv[j] = i < m ? cov[lv.full + i] : 0;
-                ev[j] = i < m ? ent[lv.full + i] : 0.0;
+                cv[j] = cov[lv.full + (i < m ? i : 0)];
             }
-#pragma unroll
-            for (int j = 0; j < kNpBuf / kTailThreads; ++j) {
-                const int i = t + kTailThreads * j;
-                cs += cv[j];
-                nz += cv[j] != 0;
-                if (i < m) s_ent[i] = ev[j];
-            }
-            __syncthreads();
-            const double e = pw_block(s_ent, m, s_off, s_len, s_val);
+            TAIL_STAMP(2);
+            const double e = pw_fast<kTailThreads>(ent + lv.full, m, s_val);
             if (t == 0) s += e;
+#pragma unroll
+            for (int j = 0; j < kNpBuf / kTailThreads; ++j) {
+                const bool in = t + kTailThreads * j < m;
+                cs += in ? cv[j] : 0;
+                nz += (in && cv[j] != 0) ? 1 : 0;
+            }
+            TAIL_STAMP(3);
         }
         cs = block_sum_i64(cs, s_red);
         nz = block_sum_i64(nz, s_red);
@@ -1259,6 +1350,7 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
         }
         return;
     }
+    TAIL_STAMP(0);
     const int w = (int)blockIdx.x / 3, q = (int)blockIdx.x % 3;
     int64_t lo = lo_a[w], hi = hi_a[w];
     if (lo < 0) lo = 0;
@@ -1280,33 +1372,58 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
     double mean;
     if (n <= kTailWin) {  // (uniform)
         const bool in = t < n;
-        const unsigned long long x = in ? key(t) : 0ull;
-        if (in) s_key[t] = x;
+        const unsigned long long x = in ? key(t) : ~0ull;  // (the pads never smaller than a key)
+        s_key[t] = x;
         if (t < 2) s_sel[t] = 0ull;
+        unsigned long long v[1] = {x};
+        wave_bitonic<1>(v);  // each wave's keys sorted by shuffles
+        s_run[t] = v[0];
         __syncthreads();
+        TAIL_STAMP(1);
         // the keys smaller than x: x <= (k-th smallest) iff at most k keys are smaller, so the
-        // k-th smallest is the largest such x
-        // (broadcast reads, 16 issued before they are compared: one LDS round trip per 16 keys)
+        // k-th smallest is the largest such x.  Counted by a branchless binary search in every
+        // wave's sorted run, the eight searches interleaved (an all-pairs compare loop cost 10k
+        // cycles of 64-bit VALU compares per window)
+        // (by the waves that hold keys; the runs past n hold pads only, counted 0, and a guard on
+        // them compiled to a branch and a wait per read)
+        const int nr = (int)((n + 63) / 64);
         int lt = 0;
-        for (int j0 = 0; j0 < n; j0 += 16) {
-            unsigned long long y[16];
+        if (wave < nr) {
+            int p[NW];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) y[u] = j0 + u < n ? s_key[j0 + u] : ~0ull;
+            for (int r = 0; r < NW; ++r) p[r] = 0;
 #pragma unroll
-            for (int u = 0; u < 16; ++u) lt += y[u] < x ? 1 : 0;
+            for (int st = 32; st > 0; st >>= 1)
+#pragma unroll
+                for (int r = 0; r < NW; ++r) p[r] += s_run[64 * r + p[r] + st - 1] < x ? st : 0;
+#pragma unroll
+            for (int r = 0; r < NW; ++r) lt += p[r] + (s_run[64 * r + p[r]] < x ? 1 : 0);
         }
-        if (in && lt <= k1) atomicMax(&s_sel[0], x);
-        if (in && lt <= k2) atomicMax(&s_sel[1], x);
+        // the largest candidate of each wave (shuffles), then one LDS max per wave (an atomicMax of
+        // every lane compiled to a scalar loop over the lanes, ~10 us per window)
+        unsigned long long c1 = (in && lt <= k1) ? x : 0ull, c2 = (in && lt <= k2) ? x : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long d1 = __shfl_xor(c1, o), d2 = __shfl_xor(c2, o);
+            c1 = d1 > c1 ? d1 : c1;
+            c2 = d2 > c2 ? d2 : c2;
+        }
+        if (lane == 0) {
+            atomicMax(&s_sel[0], c1);
+            atomicMax(&s_sel[1], c2);
+        }
+        TAIL_STAMP(2);
         if (q == 0) {  // (uniform) the exact integer sum
             long long cs = in ? (long long)x : 0;
             cs = block_sum_i64(cs, s_red);  // (contains the barriers after the rank writes)
             mean = (double)cs / (double)n;
         } else {  // numpy's pairwise mean over the window (values in LDS, as doubles)
             __syncthreads();
-            mean = pw_block((const double*)s_key, (int)n, s_off, s_len, s_val) / (double)n;
+            mean = pw_fast<kTailThreads>((const double*)s_key, (int)n, s_val) / (double)n;
         }
         a = s_sel[0];
         b = s_sel[1];
+        TAIL_STAMP(3);
     } else {  // a long window: radix selects
         const int bits = q == 0 ? 32 : 64;
         a = radix_select(key, n, k1, bits, s_hist, s_sel);
@@ -1463,8 +1580,7 @@ hipError_t launch_tail(hipStream_t s, const int32_t* cov, const double* ent, con
                        double* out, const int64_t* lo, const int64_t* hi, int n_tiles, double* amp) {
     if (L <= 0) return hipSuccess;
     const Leaves lv = summary_leaves(work, L);
-    const size_t tail_lds = (size_t)(L - lv.full) * sizeof(double);
-    hipLaunchKernelGGL(k_tail, dim3((unsigned)(3 * n_tiles + 1)), dim3(kTailThreads), tail_lds, s, cov, ent, sec, L, lo, hi,
+    hipLaunchKernelGGL(k_tail, dim3((unsigned)(3 * n_tiles + 1)), dim3(kTailThreads), 0, s, cov, ent, sec, L, lo, hi,
                        n_tiles, amp, lv, out);
     return hipGetLastError();
 }

@@ -347,7 +347,24 @@ __global__ __launch_bounds__(64 * K) void k_stats(int32_t* __restrict__ hist, in
 // are two of numpy's 128-position pairwise leaves when they lie in a whole 8192-position buffer,
 // and the block also writes each leaf's entropy sum (eight strided accumulators, added in
 // numpy's order), its exact coverage sum and its non-zero count, so no summary pass re-reads
-// the entropies (k_tail adds the leaves up the buffer's tree).
+// the entropies (k_tail adds the leaves up the buffer's tree).  The last, partial buffer's blocks
+// are its 64 nodes of numpy's tree one level above the leaves (pw_node: each <= 256 positions,
+// contiguous, together all of [full, L)), one block per node: the block's positions are the
+// node's, and it writes the node's sum -- its leaf, or its two leaves added -- so k_tail adds the
+// partial buffer up the same way as a whole one, from 64 values.
+constexpr int kLv = 7;  // 8192 -> 4096 -> ... -> 128: six splits; one spare level
+__device__ __forceinline__ void pw_node(int m, int level, int idx, int& off, int& len) {
+    // node idx of the given level (level 0: the root) of numpy's recursion over m elements
+    // (branch-free: an unsplit node is its own left child, n2 = len, and an empty right one)
+    off = 0;
+    len = m;
+    for (int l = 0; l < level; ++l) {
+        const int bit = (idx >> (level - 1 - l)) & 1;
+        const int n2 = len > 128 ? (len >> 1) & ~7 : len;  // numpy: n/2 less its remainder mod 8
+        off += bit ? n2 : 0;
+        len = bit ? len - n2 : n2;
+    }
+}
 struct Leaves {
     double* ent;  // [full buffers * 64]
     long long* cov;
@@ -360,8 +377,16 @@ __global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, 
                                                     double* __restrict__ pc, double* __restrict__ ent,
                                                     double* __restrict__ sec, Leaves lv = Leaves{}) {
     __shared__ __attribute__((aligned(16))) double tab[64][4];
-    const int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool in = P < L;
+    int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool in = P < L;
+    int node = -1, n6 = 0;  // LEAVES: a block of the partial buffer: its node and the node's length
+    if (LEAVES && (int64_t)blockIdx.x >= lv.full / 256) {  // (uniform)
+        node = (int)(blockIdx.x - lv.full / 256);
+        int o6;
+        pw_node((int)(L - lv.full), kLv - 1, node, o6, n6);
+        P = lv.full + o6 + threadIdx.x;
+        in = (int)threadIdx.x < n6;
+    }
     uint32_t c[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) c[j] = in ? (uint32_t)hist[(int64_t)j * L + P] : 0u;
@@ -415,7 +440,40 @@ __global__ __launch_bounds__(256) void k_stats_lane(int32_t* __restrict__ hist, 
         if (ent) ent[P] = h;
         if (sec) sec[P] = h2;
     }
-    if (LEAVES && (int64_t)blockIdx.x * 256 + 256 <= lv.full) {  // (uniform) two whole leaves
+    if (LEAVES && node >= 0) {  // (uniform) a node of the partial buffer: its leaf or two
+        __shared__ double s_n[256];
+        __shared__ long long s_q[8];
+        const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+        s_n[t] = h;
+        long long cs = cov, nzc = cov != 0;  // (0 past the node)
+        for (int o = 32; o > 0; o >>= 1) {
+            cs += __shfl_down(cs, o);
+            nzc += __shfl_down(nzc, o);
+        }
+        if (lane == 0) s_q[wave] = cs, s_q[4 + wave] = nzc;
+        __syncthreads();
+        if (t < 16) {  // leaf t >> 3 (left, right), accumulator j = t & 7, numpy's pairwise_sum
+            const int n2 = n6 > 128 ? (n6 >> 1) & ~7 : n6, j = t & 7;
+            const int lo = (t >> 3) ? n2 : 0, len = (t >> 3) ? n6 - n2 : n2, full = len & ~7;
+            const double* a = s_n + lo;
+            double r = a[j < full ? j : 0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) r = r + (j + 8 * i < full ? a[j + 8 * i] : -0.0);  // (-0.0: adds nothing)
+            r = r + __shfl_down(r, 1);
+            r = r + __shfl_down(r, 2);
+            r = r + __shfl_down(r, 4);
+            if (len < 8) r = 0.0;  // numpy: n < 8 sums from 0, in order
+#pragma unroll
+            for (int u = 0; u < 7; ++u) r = r + (full + u < len ? a[full + u] : -0.0);
+            const double right = __shfl_down(r, 8);
+            if (t == 0) {
+                const int64_t f = lv.full / kNpBuf * 64 + node;
+                lv.ent[f] = n6 > 128 ? r + right : r;
+                lv.cov[f] = s_q[0] + s_q[1] + s_q[2] + s_q[3];
+                lv.nz[f] = s_q[4] + s_q[5] + s_q[6] + s_q[7];
+            }
+        }
+    } else if (LEAVES && (int64_t)blockIdx.x * 256 + 256 <= lv.full) {  // (uniform) two whole leaves
         __shared__ double s_h[256];
         __shared__ long long s_r[8];
         const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -560,7 +618,6 @@ __device__ double pw_leaf(const double* a, int n) {
 // leaves are summed in parallel, then every level adds its children bottom-up: the same sums in
 // the same order as the recursion, with no per-thread stack (a private array there lives in
 // scratch memory, one slow round trip per push).  Returns the value in thread 0 only.
-constexpr int kLv = 7;  // 8192 -> 4096 -> ... -> 128: six splits; one spare level
 __device__ double pw_block(const double* a, int m, int* s_off, int* s_len, double* s_val) {
     // s_off / s_len: (2^(kLv+1) - 1) nodes; s_val: 2 x 2^kLv values (ping-pong)
     const int t = threadIdx.x;
@@ -616,18 +673,6 @@ __device__ double pw_block(const double* a, int m, int* s_off, int* s_len, doubl
 // lanes up (a shuffle down), and each lane's descent recorded which of its ancestors split.
 // a: m <= 8192 doubles (LDS or global); s_leaf: 2^kLv doubles of LDS; NT threads (all call).
 // Returns the value in thread 0 only.
-__device__ __forceinline__ void pw_node(int m, int level, int idx, int& off, int& len) {
-    // node idx of the given level (level 0: the root) of numpy's recursion over m elements
-    // (branch-free: an unsplit node is its own left child, n2 = len, and an empty right one)
-    off = 0;
-    len = m;
-    for (int l = 0; l < level; ++l) {
-        const int bit = (idx >> (level - 1 - l)) & 1;
-        const int n2 = len > 128 ? (len >> 1) & ~7 : len;  // numpy: n/2 less its remainder mod 8
-        off += bit ? n2 : 0;
-        len = bit ? len - n2 : n2;
-    }
-}
 template <int NT>
 __device__ __forceinline__ double pw_fast(const double* a, int m, double* s_leaf) {
     constexpr int kSlots = 1 << kLv, R = 8 * kSlots / NT;
@@ -1263,13 +1308,15 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 // ---- the fused --summarise-with-bed tail (main.py:469-551) after kernel 1 + 2 -------------------
 // One launch: blocks [0, 3 n_tiles) take one (amplicon window, array) each -- array 0 coverage,
 // 1 entropy, 2 secondary entropy: its numpy mean and np.median -- and the last block the summary:
-// every whole buffer's 64 leaves (k_stats_lane<LEAVES>) added up numpy's tree by a wave, the
-// buffers folded in order, the last partial buffer's pairwise sum from LDS (pw_block), the exact
-// coverage sum and non-zero count.  The windows' medians: a window of <= 512 positions is staged
-// in LDS, one element per thread, and each thread counts the keys smaller than its own: the
-// k-th smallest value is the largest one with at most k smaller keys (an LDS atomic max), so the
-// middle elements need one compare per key pair and no sort; longer windows take the radix
-// select.  Same values as k_amplicon + k_sum_chunks + k_sum_final.
+// every buffer's 64 partials (k_stats_lane<LEAVES>: a whole buffer's 128-position leaves, the
+// partial buffer's nodes one level above its leaves) added up numpy's tree by a wave, the
+// buffers folded in order, the exact coverage sum and non-zero count.  The windows' medians: a
+// window of <= 512 positions is loaded one element per thread, each wave sorts its 64 keys
+// (shuffles), and each thread counts the keys smaller than its own by a binary search in every
+// wave's sorted run: the k-th smallest value is the largest one with at most k smaller keys (a
+// wave max, then an LDS atomic max); longer windows take the radix select.  The means: numpy's
+// pairwise sum (pw_fast) over the window in LDS.  Same values as k_amplicon + k_sum_chunks +
+// k_sum_final.
 #ifdef BC_TAIL_TRACE  // diagnostic: block 0's phase stamps (s_memtime) after the windows' outputs
 #define TAIL_STAMP(k) \
     do { if (blockIdx.x == 0 && threadIdx.x == 0) amp[6 * n_tiles + (k)] = (double)__builtin_amdgcn_s_memtime(); } while (0)
@@ -1293,52 +1340,45 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if ((int)blockIdx.x == 3 * n_tiles) {  // (uniform) the summary
         TAIL_STAMP(0);
-        const int64_t nfull = lv.full / kNpBuf;
+        // the partial buffer's tree above its 64 nodes: which of lane's ancestors split
+        const int m = (int)(L - lv.full);
+        unsigned split = 0;
+        {
+            int n = m;
+#pragma unroll
+            for (int l = 0; l < kLv - 1; ++l) {
+                split |= (unsigned)(n > 128) << l;
+                const int n2 = n > 128 ? (n >> 1) & ~7 : n;
+                n = ((lane >> (kLv - 2 - l)) & 1) ? n - n2 : n2;
+            }
+        }
+        const int64_t nfull = lv.full / kNpBuf, nbuf = nfull + (m > 0);
         double s = 0.0;
         long long cs = 0, nz = 0;
-        for (int64_t b0 = 0; b0 < nfull; b0 += NW) {
+        for (int64_t b0 = 0; b0 < nbuf; b0 += NW) {
             const int64_t b = b0 + wave;
             double v = 0.0;
-            if (b < nfull) {
+            if (b < nbuf) {
                 const int64_t f = b * 64 + lane;
                 v = lv.ent[f];
                 cs += lv.cov[f];
                 nz += lv.nz[f];
             }
-            // numpy's tree over a buffer's 64 leaves: neighbours first (pw_full8192's order)
-            v = v + __shfl_down(v, 1);
-            v = v + __shfl_down(v, 2);
-            v = v + __shfl_down(v, 4);
-            v = v + __shfl_down(v, 8);
-            v = v + __shfl_down(v, 16);
-            v = v + __shfl_down(v, 32);
+            // numpy's tree over a buffer's 64 nodes: node i of level d in lane i << (6 - d), its
+            // right child 2^(5-d) lanes up; a whole buffer splits everywhere (pw_full8192's order)
+            const unsigned sp = b < nfull ? ~0u : split;
+#pragma unroll
+            for (int d = kLv - 2; d >= 0; --d) {
+                const double c1 = __shfl_down(v, 1 << (kLv - 2 - d));
+                v = ((sp >> d) & 1) ? v + c1 : v;
+            }
             if (lane == 0) s_buf[wave] = v;
             __syncthreads();
             if (t == 0)
-                for (int w = 0; w < NW && b0 + w < nfull; ++w) s += s_buf[w];  // buffers in order
+                for (int w = 0; w < NW && b0 + w < nbuf; ++w) s += s_buf[w];  // buffers in order
             __syncthreads();
         }
         TAIL_STAMP(1);
-        const int m = (int)(L - lv.full);  // the last, partial buffer: [full, L)
-        if (m > 0) {
-            // its coverage loads issued first, then its pairwise sum straight from the array
-            int cv[kNpBuf / kTailThreads];
-#pragma unroll
-            for (int j = 0; j < kNpBuf / kTailThreads; ++j) {
-                const int i = t + kTailThreads * j;
-                cv[j] = cov[lv.full + (i < m ? i : 0)];
-            }
-            TAIL_STAMP(2);
-            const double e = pw_fast<kTailThreads>(ent + lv.full, m, s_val);
-            if (t == 0) s += e;
-#pragma unroll
-            for (int j = 0; j < kNpBuf / kTailThreads; ++j) {
-                const bool in = t + kTailThreads * j < m;
-                cs += in ? cv[j] : 0;
-                nz += (in && cv[j] != 0) ? 1 : 0;
-            }
-            TAIL_STAMP(3);
-        }
         cs = block_sum_i64(cs, s_red);
         nz = block_sum_i64(nz, s_red);
         if (t == 0) {
@@ -1566,7 +1606,7 @@ hipError_t launch_stats_leaves(hipStream_t s, int32_t* hist, int64_t L, int k, d
                                double* ent, double* sec, int32_t* counts_out, void* work) {
     if (L <= 0) return hipSuccess;
     const Leaves lv = summary_leaves(work, L);
-    const unsigned lb = (unsigned)((L + 255) / 256);
+    const unsigned lb = (unsigned)(lv.full / 256 + (L > lv.full ? 64 : 0));  // + the partial buffer's nodes
     if (k == 5)
         hipLaunchKernelGGL((k_stats_lane<5, true>), dim3(lb), dim3(256), 0, s, hist, L, nf, nf2, counts_out, cov,
                            nullptr, ent, sec, lv);

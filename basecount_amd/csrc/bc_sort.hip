@@ -445,70 +445,70 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(SortArgs A) {
     for (int h = threadIdx.x; h < H; h += kBktThreads) A.mat[(int64_t)blockIdx.x * H + h] = hist[h];
 }
 
+// Every bucket's total and its reads in blocks before b, added into next / pre (LDS, zeroed):
+// wave v takes rows v, v + 16, ..., R of them per round, lane the buckets lane + 64 m, m < G
+// (every load of a round issued before its adds); the 16 waves' partial sums meet in LDS.  The
+// rows were written by blocks on every XCD, so each round is a trip past this XCD's L2.
+template <int G, int R>
+__device__ __forceinline__ void count_rows(const SortArgs& A, int b, uint32_t* next, uint32_t* pre) {
+    const int H = A.nbkt, nb = A.nblk;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int NW = kBktThreads / 64;
+    for (int h0 = 0; h0 < H; h0 += 64 * G) {
+        uint32_t tot[G], before[G];
+#pragma unroll
+        for (int m = 0; m < G; ++m) tot[m] = 0u, before[m] = 0u;
+        for (int r0 = wave; r0 < nb; r0 += NW * R) {
+            uint32_t v[R][G];
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+#pragma unroll
+                for (int m = 0; m < G; ++m) {
+                    const int r = r0 + u * NW, h = h0 + 64 * m + lane;
+                    v[u][m] = r < nb && h < H ? A.mat[(int64_t)r * H + h] : 0u;
+                }
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+#pragma unroll
+                for (int m = 0; m < G; ++m) {
+                    tot[m] += v[u][m];
+                    before[m] += r0 + u * NW < b ? v[u][m] : 0u;
+                }
+        }
+#pragma unroll
+        for (int m = 0; m < G; ++m) {
+            const int h = h0 + 64 * m + lane;
+            if (h < H && tot[m]) atomicAdd(&next[h], tot[m]);
+            if (h < H && before[m]) atomicAdd(&pre[h], before[m]);
+        }
+    }
+}
+
 template <bool FIELDS>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     __shared__ uint32_t next[kBktMax], pre[kBktMax];
     __shared__ __attribute__((aligned(16))) uint32_t dscr[(FIELDS && kSortRuns) ? 8 * kBktThreads : 4];
+    __shared__ uint32_t lcnt[(FIELDS && kSortRuns) ? 1 : kBktMax];  // a round's bucket counts, scanned
+    __shared__ uint4 stage[(FIELDS && kSortRuns) ? 1 : 4 * kBktThreads];  // a round's records by bucket
     __shared__ uint32_t ws[kBktThreads / 64];
     __shared__ uint32_t rq, rf;
-    const int H = A.nbkt, nb = A.nblk, b = blockIdx.x;
+    const int H = A.nbkt, b = blockIdx.x;
     if (threadIdx.x == 0) rq = 0u, rf = 0u;  // the block's largest query length and flags
     const int64_t beg = (int64_t)b * A.chunk;
     const int64_t end = beg + A.chunk < A.n ? beg + A.chunk : A.n;
-    // bucket h's total and its reads in blocks before b, from the count rows: wave v takes rows
-    // v, v + 16, ..., lane the buckets lane + 64 m (every load of a lane issued before its adds),
-    // the 16 waves' partial sums meet in LDS
-    for (int h = threadIdx.x; h < H; h += kBktThreads) next[h] = 0u, pre[h] = 0u;
-    __syncthreads();
-    {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        constexpr int NW = kBktThreads / 64;
-        for (int h0 = 0; h0 < H; h0 += 64 * kBktGroup) {
-            uint32_t tot[kBktGroup], before[kBktGroup];
-#pragma unroll
-            for (int m = 0; m < kBktGroup; ++m) tot[m] = 0u, before[m] = 0u;
-            for (int r0 = wave; r0 < nb; r0 += NW * kBktRows) {
-                uint32_t v[kBktRows][kBktGroup];
-#pragma unroll
-                for (int u = 0; u < kBktRows; ++u)
-#pragma unroll
-                    for (int m = 0; m < kBktGroup; ++m) {
-                        const int r = r0 + u * NW, h = h0 + 64 * m + lane;
-                        v[u][m] = r < nb && h < H ? A.mat[(int64_t)r * H + h] : 0u;
-                    }
-#pragma unroll
-                for (int u = 0; u < kBktRows; ++u)
-#pragma unroll
-                    for (int m = 0; m < kBktGroup; ++m) {
-                        tot[m] += v[u][m];
-                        before[m] += r0 + u * NW < b ? v[u][m] : 0u;
-                    }
-            }
-#pragma unroll
-            for (int m = 0; m < kBktGroup; ++m) {
-                const int h = h0 + 64 * m + lane;
-                if (h < H && tot[m]) atomicAdd(&next[h], tot[m]);
-                if (h < H && before[m]) atomicAdd(&pre[h], before[m]);
-            }
-        }
-    }
-    __syncthreads();
-    lds_scan_excl<kBktThreads, kBktMax / kBktThreads>(next, H, ws);
-    if (b == 0) {  // every bucket's first slot, for the rank pass
-        for (int h = threadIdx.x; h < H; h += kBktThreads) A.bbase[h] = next[h];
-        if (threadIdx.x == 0) A.bbase[H] = (uint32_t)A.n;
-    }
-    for (int h = threadIdx.x; h < H; h += kBktThreads) next[h] += pre[h];
-    __syncthreads();
     constexpr int B = 4;  // reads per thread whose loads are in flight together
+    constexpr bool kStaged = !(FIELDS && kSortRuns);
     uint32_t qm = 0, fl = 0;
-    for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)B * kBktThreads) {
-        uint32_t p[B], cb[B], cn[B], sn[B];
+    const int t = threadIdx.x;
+    uint32_t p[B], cb[B], cn[B], sn[B];
+    bool in[B];
+    auto load_round = [&](int64_t r0) {  // the fields of a round's reads
 #pragma unroll
         for (int u = 0; u < B; ++u) {
-            const int64_t i = i0 + (int64_t)u * kBktThreads;
+            const int64_t i = r0 + t + (int64_t)u * kBktThreads;
+            in[u] = i < end;
             p[u] = 0u, cb[u] = 0u, cn[u] = 0u, sn[u] = 0u;
-            if (i < end) {
+            if (in[u]) {
                 bool bad;
                 p[u] = bkt_pos(A, i, bad);
                 fl |= bad ? 2u : 0u;
@@ -517,21 +517,106 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
                 sn[u] = A.seq_nib[i];
             }
         }
-        if (FIELDS && !kSortRuns) {  // the record alone
+    };
+    // bucket h's total and its reads in blocks before b, from the count rows (count_rows)
+    for (int h = threadIdx.x; h < H; h += kBktThreads) next[h] = 0u, pre[h] = 0u;
+    __syncthreads();
+    if (H <= 256)  // (uniform) C3's 234 buckets x 245 rows: every load of a lane in one round trip
+        count_rows<4, 16>(A, b, next, pre);
+    else
+        count_rows<kBktGroup, kBktRows>(A, b, next, pre);
+    __syncthreads();
+    lds_scan_excl<kBktThreads, kBktMax / kBktThreads>(next, H, ws);
+    if (b == 0) {  // every bucket's first slot, for the rank pass
+        for (int h = threadIdx.x; h < H; h += kBktThreads) A.bbase[h] = next[h];
+        if (threadIdx.x == 0) A.bbase[H] = (uint32_t)A.n;
+    }
+    for (int h = threadIdx.x; h < H; h += kBktThreads) next[h] += pre[h];
+    __syncthreads();
+    if constexpr (kStaged) {
+        // Rounds of B x kBktThreads reads: each read's record placed in LDS by bucket (the round's
+        // counts, scanned), then the block writes the round bucket run by bucket run, neighbouring
+        // slots from neighbouring lanes.  (A store per record straight to its slot scattered the
+        // 16-byte records over every bucket: 18.5 us at C3.)
+        // (the first round's loads issued before the count rows' instead: 19.7 vs 17.1 us)
+        for (int64_t r0 = beg; r0 < end; r0 += (int64_t)B * kBktThreads) {
+            load_round(r0);
+            uint4 rec[B];
+            if (FIELDS) {
+#pragma unroll
+                for (int u = 0; u < B; ++u) rec[u] = make_uint4(p[u], cb[u], sn[u], cn[u]);
+            } else {
+                uint32_t w[B][8];
+#pragma unroll
+                for (int u = 0; u < B; ++u)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) w[u][k] = (uint32_t)k < cn[u] ? A.cigar[cb[u] + k] : 0u;
+#pragma unroll
+                for (int u = 0; u < B; ++u) {
+                    uint32_t q = 0;  // query length (M/I/=/X)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (qcons(w[u][k] & 15u)) q += w[u][k] >> 4;
+                    for (uint32_t k = 8; k < cn[u]; ++k) {
+                        const uint32_t x = A.cigar[cb[u] + k];
+                        if (qcons(x & 15u)) q += x >> 4;
+                    }
+                    qm = (in[u] && q > qm) ? q : qm;
+                    // cig_n and the query length packed in 16 bits each; a read that needs more
+                    // (only a caller's batch: BAM's n_cigar_op is 16 bits) keeps its source
+                    // index for the copy
+                    const bool small = cn[u] <= 0xFFFFu && q < kQlenMax;
+                    const int64_t i = r0 + t + (int64_t)u * kBktThreads;
+                    rec[u] = make_uint4(p[u], cb[u], small ? sn[u] : (uint32_t)i, small ? cn[u] | q << 16 : kBigRec);
+                }
+            }
+            uint32_t bk[B];
+            bool inr[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) bk[u] = p[u] >> A.wbits, inr[u] = in[u];
+            for (int h = t; h < H; h += kBktThreads) lcnt[h] = 0u;
+            __syncthreads();
+            uint32_t rk[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) rk[u] = inr[u] ? atomicAdd(&lcnt[bk[u]], 1u) : 0u;
+            __syncthreads();
+            lds_scan_excl<kBktThreads, kBktMax / kBktThreads>(lcnt, H, ws);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (inr[u]) stage[lcnt[bk[u]] + rk[u]] = rec[u];
+            __syncthreads();
+            const int nr = (int)(end - r0 < (int64_t)B * kBktThreads ? end - r0 : (int64_t)B * kBktThreads);
+            for (int i = t; i < nr; i += kBktThreads) {
+                const uint4 x = stage[i];
+                const uint32_t h = x.x >> A.wbits;
+                A.brec[next[h] + (uint32_t)i - lcnt[h]] = x;
+            }
+            __syncthreads();
+            for (int h = t; h < H; h += kBktThreads) next[h] += (h + 1 < H ? lcnt[h + 1] : (uint32_t)nr) - lcnt[h];
+            __syncthreads();
+        }
+    } else {
+        for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)B * kBktThreads) {
+            uint32_t p[B], cb[B], cn[B], sn[B];
 #pragma unroll
             for (int u = 0; u < B; ++u) {
                 const int64_t i = i0 + (int64_t)u * kBktThreads;
-                if (i >= end) break;
-                A.brec[atomicAdd(&next[p[u] >> A.wbits], 1u)] = make_uint4(p[u], cb[u], sn[u], cn[u]);
+                p[u] = 0u, cb[u] = 0u, cn[u] = 0u, sn[u] = 0u;
+                if (i < end) {
+                    bool bad;
+                    p[u] = bkt_pos(A, i, bad);
+                    fl |= bad ? 2u : 0u;
+                    cb[u] = A.cig_beg[i];
+                    cn[u] = A.cig_n[i];
+                    sn[u] = A.seq_nib[i];
+                }
             }
-            continue;
-        }
-        uint32_t w[B][8];
+            uint32_t w[B][8];
 #pragma unroll
-        for (int u = 0; u < B; ++u)
+            for (int u = 0; u < B; ++u)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) w[u][k] = (uint32_t)k < cn[u] ? A.cigar[cb[u] + k] : 0u;
-        if (FIELDS) {  // no copy: the record and the read's run record (k_rc then decodes nothing)
+                for (int k = 0; k < 8; ++k) w[u][k] = (uint32_t)k < cn[u] ? A.cigar[cb[u] + k] : 0u;
+            // no copy: the record and the read's run record (k_rc then decodes nothing)
             int cm[B];
 #pragma unroll
             for (int u = 0; u < B; ++u)  // ops decoded: the wave's longest CIGAR (up to kPre), outside the tail's branch
@@ -552,26 +637,6 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
                 A.brec[j] = make_uint4(p[u], cb[u], sn[u], cn[u]);
                 A.brun[j] = make_uint4(rr[0], rr[1], rr[2], rr[3]);
             }
-            continue;
-        }
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            const int64_t i = i0 + (int64_t)u * kBktThreads;
-            if (i >= end) break;
-            uint32_t q = 0;  // query length (M/I/=/X)
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (qcons(w[u][k] & 15u)) q += w[u][k] >> 4;
-            for (uint32_t k = 8; k < cn[u]; ++k) {
-                const uint32_t x = A.cigar[cb[u] + k];
-                if (qcons(x & 15u)) q += x >> 4;
-            }
-            qm = q > qm ? q : qm;
-            const uint32_t j = atomicAdd(&next[p[u] >> A.wbits], 1u);
-            // cig_n and the query length packed in 16 bits each; a read that needs more (only a
-            // caller's batch: BAM's n_cigar_op is 16 bits) keeps its source index for the copy
-            const bool small = cn[u] <= 0xFFFFu && q < kQlenMax;
-            A.brec[j] = make_uint4(p[u], cb[u], small ? sn[u] : (uint32_t)i, small ? cn[u] | q << 16 : kBigRec);
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -590,11 +655,11 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(SortArgs A) {
     }
 }
 
-constexpr int kPermSlots = 1024;  // fields-only rank: sorted slots per LDS pass (32 KiB)
+constexpr int kPermSlots = kSortRuns ? 1024 : 4096;  // fields-only rank: sorted slots per LDS pass (16 B each, + 16 B of run)
 template <bool FIELDS>
 __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
     __shared__ uint32_t cnt[kBktLowMax];
-    __shared__ uint4 perm_rec[FIELDS ? kPermSlots : 1], perm_run[FIELDS ? kPermSlots : 1];
+    __shared__ uint4 perm_rec[FIELDS ? kPermSlots : 1], perm_run[(FIELDS && kSortRuns) ? kPermSlots : 1];
     __shared__ uint32_t ws[kRankThreads / 64];
     __shared__ uint32_t rq, rf;
     const int h = blockIdx.x, t = threadIdx.x;
@@ -671,11 +736,11 @@ __global__ __launch_bounds__(kRankThreads) void k_bkt_rank(SortArgs A) {
             for (int k = 0; k < kRankRegs; ++k)
                 if (lr[k] - p0 < (uint32_t)kPermSlots) {
                     perm_rec[lr[k] - p0] = rec[k];
-                    if (kSortRuns) perm_run[lr[k] - p0] = run[FIELDS ? k : 0];
+                    if constexpr (kSortRuns) perm_run[lr[k] - p0] = run[FIELDS ? k : 0];
                 }
             __syncthreads();
             for (uint32_t q = t; q < kPermSlots && p0 + q < be - bs; q += kRankThreads)
-                put(bs + p0 + q, perm_rec[q], perm_run[q]);
+                put(bs + p0 + q, perm_rec[q], perm_run[kSortRuns ? q : 0]);
             __syncthreads();
         }
         return;

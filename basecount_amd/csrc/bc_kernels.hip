@@ -665,71 +665,71 @@ __device__ double pw_block(const double* a, int m, int* s_off, int* s_len, doubl
 }
 
 // The same sum, pw_block's tree, without its 14 barriers and one-thread leaves: every leaf slot
-// (kLv levels of numpy's split: a leaf passes itself down as the left child, an empty right one)
+// (LV levels of numpy's split: a leaf passes itself down as the left child, an empty right one)
 // is found by descending its bit path, its eight strided accumulators are eight threads'
 // (every load issued together, unguarded: clamped, and the extra ones selected to -0.0, which
 // adds exactly nothing to any double), combined by shuffles in numpy's order; then one wave adds
-// the slots up the tree: node i of level d sits in lane i << (6 - d), its right child 2^(5-d)
-// lanes up (a shuffle down), and each lane's descent recorded which of its ancestors split.
-// a: m <= 8192 doubles (LDS or global); s_leaf: 2^kLv doubles of LDS; NT threads (all call).
-// Returns the value in thread 0 only.
-template <int NT>
+// the slots up the tree: node i of level d sits in lane i << (LV - 1 - d), its right child
+// 2^(LV-2-d) lanes up (a shuffle down), and each lane's descent recorded which of its ancestors
+// split.  LV = kLv covers m <= 8192; LV = 4 covers m <= 512 (checked against numpy for every
+// such m) with 128 tasks, two waves, instead of 1024.  a: m doubles (LDS or global); s_leaf:
+// 2^LV doubles of LDS; NT threads, all calling.  Returns the value in thread 0 only.
+template <int NT, int LV = kLv>
 __device__ __forceinline__ double pw_fast(const double* a, int m, double* s_leaf) {
-    constexpr int kSlots = 1 << kLv, R = 8 * kSlots / NT;
-    static_assert(R * NT == 8 * kSlots, "NT must divide 8 x 2^kLv");
+    constexpr int kSlots = 1 << LV, kTasks = 8 * kSlots, R = kTasks >= NT ? kTasks / NT : 1;
+    static_assert(kTasks % 64 == 0 && (kTasks < NT || R * NT == kTasks), "tasks: whole waves");
     const int t = threadIdx.x, j = t & 7;  // (NT is a multiple of 8: every task of a thread has accumulator j)
-    int len[R], full[R];
-    double v[R][16], rem[R][7];
+    if (kTasks >= NT || t < kTasks) {  // (wave-uniform)
+        int len[R], full[R];
+        double v[R][16], rem[R][7];
 #pragma unroll
-    for (int q = 0; q < R; ++q) {  // every task's loads issued first
-        int off;
-        pw_node(m, kLv, (t + NT * q) >> 3, off, len[q]);
-        full[q] = len[q] & ~7;
+        for (int q = 0; q < R; ++q) {  // every task's loads issued first
+            int off;
+            pw_node(m, LV, (t + NT * q) >> 3, off, len[q]);
+            full[q] = len[q] & ~7;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int i = j + 8 * u;
-            v[q][u] = a[off + (i < full[q] ? i : 0)];
+            for (int u = 0; u < 16; ++u) {
+                const int i = j + 8 * u;
+                v[q][u] = a[off + (i < full[q] ? i : 0)];
+            }
+#pragma unroll
+            for (int u = 0; u < 7; ++u) {  // the leaf's last len % 8 (or, below 8, all) elements
+                const int i = full[q] + u;
+                rem[q][u] = a[off + (i < len[q] ? i : 0)];
+            }
         }
 #pragma unroll
-        for (int u = 0; u < 7; ++u) {  // the leaf's last len % 8 (or, below 8, all) elements
-            const int i = full[q] + u;
-            rem[q][u] = a[off + (i < len[q] ? i : 0)];
+        for (int q = 0; q < R; ++q) {
+            double x = v[q][0];
+#pragma unroll
+            for (int u = 1; u < 16; ++u) x = x + (j + 8 * u < full[q] ? v[q][u] : -0.0);
+            x = x + __shfl_down(x, 1);  // (r0+r1), (r2+r3), ...
+            x = x + __shfl_down(x, 2);
+            x = x + __shfl_down(x, 4);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+            if (len[q] < 8) x = 0.0;    // numpy: n < 8 sums from 0, in order
+#pragma unroll
+            for (int u = 0; u < 7; ++u) x = x + (full[q] + u < len[q] ? rem[q][u] : -0.0);
+            if (((t + NT * q) & 7) == 0) s_leaf[(t + NT * q) >> 3] = x;
         }
     }
-    double r[R];
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        double x = v[q][0];
-#pragma unroll
-        for (int u = 1; u < 16; ++u) x = x + (j + 8 * u < full[q] ? v[q][u] : -0.0);
-        x = x + __shfl_down(x, 1);  // (r0+r1), (r2+r3), ...
-        x = x + __shfl_down(x, 2);
-        x = x + __shfl_down(x, 4);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
-        if (len[q] < 8) x = 0.0;    // numpy: n < 8 sums from 0, in order
-#pragma unroll
-        for (int u = 0; u < 7; ++u) x = x + (full[q] + u < len[q] ? rem[q][u] : -0.0);
-        r[q] = x;
-    }
-#pragma unroll
-    for (int q = 0; q < R; ++q)
-        if (((t + NT * q) & 7) == 0) s_leaf[(t + NT * q) >> 3] = r[q];
     __syncthreads();
     double res = 0.0;
     if (t < 64) {
-        // lane t's descent to node t of level kLv - 1, recording which ancestors split
+        // lane tt's descent to node tt of level LV - 1, recording which ancestors split
+        const int tt = t < (1 << (LV - 1)) ? t : 0;
         int n = m;
         unsigned split = 0;
 #pragma unroll
-        for (int l = 0; l < kLv - 1; ++l) {
+        for (int l = 0; l < LV - 1; ++l) {
             split |= (unsigned)(n > 128) << l;
             const int n2 = n > 128 ? (n >> 1) & ~7 : n;
-            n = ((t >> (kLv - 2 - l)) & 1) ? n - n2 : n2;
+            n = ((tt >> (LV - 2 - l)) & 1) ? n - n2 : n2;
         }
-        const double v0 = s_leaf[2 * t], v1 = s_leaf[2 * t + 1];
+        const double v0 = s_leaf[2 * tt], v1 = s_leaf[2 * tt + 1];
         double val = n > 128 ? v0 + v1 : v0;
 #pragma unroll
-        for (int d = kLv - 2; d >= 0; --d) {
-            const double c1 = __shfl_down(val, 1 << (kLv - 2 - d));
+        for (int d = LV - 2; d >= 0; --d) {
+            const double c1 = __shfl_down(val, 1 << (LV - 2 - d));
             val = ((split >> d) & 1) ? val + c1 : val;
         }
         res = val;
@@ -1323,6 +1323,21 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 #else
 #define TAIL_STAMP(k) do {} while (0)
 #endif
+// Keys below x in NR sorted runs of 64 (LDS): NR branchless binary searches, interleaved
+template <int NR>
+__device__ __forceinline__ int runs_below(const unsigned long long* run, unsigned long long x) {
+    int p[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) p[r] = 0;
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) p[r] += run[64 * r + p[r] + st - 1] < x ? st : 0;
+    int lt = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) lt += p[r] + (run[64 * r + p[r]] < x ? 1 : 0);
+    return lt;
+}
 constexpr int kTailThreads = 512;
 constexpr int kTailWin = kTailThreads;  // one position per thread
 __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const double* ent, const double* sec, int64_t L,
@@ -1424,20 +1439,21 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
         // k-th smallest is the largest such x.  Counted by a branchless binary search in every
         // wave's sorted run, the eight searches interleaved (an all-pairs compare loop cost 10k
         // cycles of 64-bit VALU compares per window)
-        // (by the waves that hold keys; the runs past n hold pads only, counted 0, and a guard on
-        // them compiled to a branch and a wait per read)
+        // (by the waves that hold keys, in the runs that hold keys: a guard per run inside one
+        // unrolled loop compiled to a branch and a wait per read)
         const int nr = (int)((n + 63) / 64);
         int lt = 0;
         if (wave < nr) {
-            int p[NW];
-#pragma unroll
-            for (int r = 0; r < NW; ++r) p[r] = 0;
-#pragma unroll
-            for (int st = 32; st > 0; st >>= 1)
-#pragma unroll
-                for (int r = 0; r < NW; ++r) p[r] += s_run[64 * r + p[r] + st - 1] < x ? st : 0;
-#pragma unroll
-            for (int r = 0; r < NW; ++r) lt += p[r] + (s_run[64 * r + p[r]] < x ? 1 : 0);
+            switch (nr) {  // (uniform; the search of nr runs unrolled at compile time)
+                case 1: lt = runs_below<1>(s_run, x); break;
+                case 2: lt = runs_below<2>(s_run, x); break;
+                case 3: lt = runs_below<3>(s_run, x); break;
+                case 4: lt = runs_below<4>(s_run, x); break;
+                case 5: lt = runs_below<5>(s_run, x); break;
+                case 6: lt = runs_below<6>(s_run, x); break;
+                case 7: lt = runs_below<7>(s_run, x); break;
+                default: lt = runs_below<8>(s_run, x); break;
+            }
         }
         // the largest candidate of each wave (shuffles), then one LDS max per wave (an atomicMax of
         // every lane compiled to a scalar loop over the lanes, ~10 us per window)
@@ -1459,7 +1475,7 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
             mean = (double)cs / (double)n;
         } else {  // numpy's pairwise mean over the window (values in LDS, as doubles)
             __syncthreads();
-            mean = pw_fast<kTailThreads>((const double*)s_key, (int)n, s_val) / (double)n;
+            mean = pw_fast<kTailThreads, 4>((const double*)s_key, (int)n, s_val) / (double)n;  // (n <= 512)
         }
         a = s_sel[0];
         b = s_sel[1];

@@ -1306,8 +1306,8 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 }
 
 // ---- the fused --summarise-with-bed tail (main.py:469-551) after kernel 1 + 2 -------------------
-// One launch: blocks [0, 3 n_tiles) take one (amplicon window, array) each -- array 0 coverage,
-// 1 entropy, 2 secondary entropy: its numpy mean and np.median -- and the last block the summary:
+// One launch: blocks 1 .. 3 n_tiles take one (amplicon window, array) each -- array 0 coverage,
+// 1 entropy, 2 secondary entropy: its numpy mean and np.median -- and block 0 the summary:
 // every buffer's 64 partials (k_stats_lane<LEAVES>: a whole buffer's 128-position leaves, the
 // partial buffer's nodes one level above its leaves) added up numpy's tree by a wave, the
 // buffers folded in order, the exact coverage sum and non-zero count.  The windows' medians: a
@@ -1317,9 +1317,9 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 // wave max, then an LDS atomic max); longer windows take the radix select.  The means: numpy's
 // pairwise sum (pw_fast) over the window in LDS.  Same values as k_amplicon + k_sum_chunks +
 // k_sum_final.
-#ifdef BC_TAIL_TRACE  // diagnostic: block 0's phase stamps (s_memtime) after the windows' outputs
+#ifdef BC_TAIL_TRACE  // diagnostic: block 1's phase stamps (s_memtime; the first window's entropy) after the windows' outputs
 #define TAIL_STAMP(k) \
-    do { if (blockIdx.x == 0 && threadIdx.x == 0) amp[6 * n_tiles + (k)] = (double)__builtin_amdgcn_s_memtime(); } while (0)
+    do { if (blockIdx.x == 1 && threadIdx.x == 0) amp[6 * n_tiles + (k)] = (double)__builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define TAIL_STAMP(k) do {} while (0)
 #endif
@@ -1353,7 +1353,10 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
     constexpr int NW = kTailThreads / 64;
     __shared__ double s_buf[NW];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    if ((int)blockIdx.x == 3 * n_tiles) {  // (uniform) the summary
+    // block 0 the summary (dispatched first: the longest chain), then the entropy blocks of every
+    // window, then the coverage ones (no pairwise mean: the lightest, so the blocks past one per
+    // CU that share a CU with another are these)
+    if (blockIdx.x == 0) {  // (uniform) the summary
         TAIL_STAMP(0);
         // the partial buffer's tree above its 64 nodes: which of lane's ancestors split
         const int m = (int)(L - lv.full);
@@ -1406,7 +1409,8 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
         return;
     }
     TAIL_STAMP(0);
-    const int w = (int)blockIdx.x / 3, q = (int)blockIdx.x % 3;
+    const int bq = (int)blockIdx.x - 1;
+    const int w = bq < 2 * n_tiles ? bq >> 1 : bq - 2 * n_tiles, q = bq < 2 * n_tiles ? 1 + (bq & 1) : 0;
     int64_t lo = lo_a[w], hi = hi_a[w];
     if (lo < 0) lo = 0;
     if (hi > L - 1) hi = L - 1;

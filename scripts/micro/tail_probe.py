@@ -38,7 +38,7 @@ for nt in (len(tiles), 0, 1, 10):
     rep = ctx.timing_report()
     ctx.timing(False)
     print(nt, "windows:", {n: round(v[1], 2) for n, v in rep.items()}, flush=True)
-    if os.environ.get("TAIL_TRACE"):  # (-DBC_TAIL_TRACE build) block 0's phase stamps (nt = 0: the fold)
+    if nt and os.environ.get("TAIL_TRACE"):  # (-DBC_TAIL_TRACE build) block 1's phase stamps
         st = damp.download(np.float64, 6 * nt + 4)[6 * nt:]
         print("  stamps (cycles from phase 0):", [int(x - st[0]) for x in st], flush=True)
 ctx.timing(True)

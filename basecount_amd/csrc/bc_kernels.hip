@@ -1173,8 +1173,8 @@ __device__ double np_mean_block(const double* a, int64_t n, int* s_off, int* s_l
 // Ascending bitonic sort of 64 * E unsigned 64-bit keys by ONE wave, E per lane (element
 // lane * E + r in register r), no barriers: pairs less than E apart are in one lane's registers,
 // the others E * m apart are lanes m apart (one 64-bit shuffle per key).  Fully unrolled.
-template <int E>
-__device__ __forceinline__ void wave_bitonic(unsigned long long (&v)[E]) {
+template <int E, typename T = unsigned long long>
+__device__ __forceinline__ void wave_bitonic(T (&v)[E]) {
     const int lane = threadIdx.x & 63;
     constexpr int N = 64 * E;
 #pragma unroll
@@ -1186,9 +1186,9 @@ __device__ __forceinline__ void wave_bitonic(unsigned long long (&v)[E]) {
                 const bool lower = (lane & m) == 0;
 #pragma unroll
                 for (int r = 0; r < E; ++r) {
-                    const unsigned long long p = __shfl_xor(v[r], m);
+                    const T p = __shfl_xor(v[r], m);
                     const bool up = ((lane * E + r) & k) == 0;
-                    const unsigned long long lo = v[r] < p ? v[r] : p, hi = v[r] < p ? p : v[r];
+                    const T lo = v[r] < p ? v[r] : p, hi = v[r] < p ? p : v[r];
                     v[r] = (up == lower) ? lo : hi;
                 }
             } else {
@@ -1196,8 +1196,8 @@ __device__ __forceinline__ void wave_bitonic(unsigned long long (&v)[E]) {
                 for (int r = 0; r < E; ++r) {
                     if (r & j) continue;
                     const bool up = ((lane * E + r) & k) == 0;
-                    const unsigned long long a = v[r], b = v[r ^ j];
-                    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+                    const T a = v[r], b = v[r ^ j];
+                    const T lo = a < b ? a : b, hi = a < b ? b : a;
                     v[r] = up ? lo : hi;
                     v[r ^ j] = up ? hi : lo;
                 }
@@ -1324,8 +1324,8 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 #define TAIL_STAMP(k) do {} while (0)
 #endif
 // Keys below x in NR sorted runs of 64 (LDS): NR branchless binary searches, interleaved
-template <int NR>
-__device__ __forceinline__ int runs_below(const unsigned long long* run, unsigned long long x) {
+template <int NR, typename T>
+__device__ __forceinline__ int runs_below(const T* run, T x) {
     int p[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) p[r] = 0;
@@ -1337,6 +1337,49 @@ __device__ __forceinline__ int runs_below(const unsigned long long* run, unsigne
 #pragma unroll
     for (int r = 0; r < NR; ++r) lt += p[r] + (run[64 * r + p[r]] < x ? 1 : 0);
     return lt;
+}
+// The k1-th and k2-th smallest of a window's n <= 512 keys, one per thread (pads ~0: never
+// smaller than a key): each wave sorts its 64 keys by shuffles, each thread counts the keys
+// below its own by a binary search in every wave's sorted run (by the waves that hold keys, in
+// the runs that hold keys: a guard per run inside one unrolled loop compiled to a branch and a
+// wait per read); x <= (k-th smallest) iff at most k keys are below x, so the k-th smallest is
+// the largest such x: a wave max (shuffles), then one LDS max per wave (an atomicMax of every
+// lane compiled to a scalar loop over the lanes, ~10 us per window) into s_sel (zeroed, read
+// after the caller's next barrier).  T: the coverage's 32 bits (half the shuffles and compares)
+// or an entropy's 64.  An all-pairs compare loop cost 10k cycles per window.
+template <typename T>
+__device__ __forceinline__ void window_kth(T x, bool in, int64_t n, int64_t k1, int64_t k2, T* s_run,
+                                           unsigned long long* s_sel) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    T v[1] = {x};
+    wave_bitonic<1, T>(v);
+    s_run[t] = v[0];
+    __syncthreads();
+    const int nr = (int)((n + 63) / 64);
+    int lt = 0;
+    if (wave < nr) {
+        switch (nr) {  // (uniform; the search of nr runs unrolled at compile time)
+            case 1: lt = runs_below<1, T>(s_run, x); break;
+            case 2: lt = runs_below<2, T>(s_run, x); break;
+            case 3: lt = runs_below<3, T>(s_run, x); break;
+            case 4: lt = runs_below<4, T>(s_run, x); break;
+            case 5: lt = runs_below<5, T>(s_run, x); break;
+            case 6: lt = runs_below<6, T>(s_run, x); break;
+            case 7: lt = runs_below<7, T>(s_run, x); break;
+            default: lt = runs_below<8, T>(s_run, x); break;
+        }
+    }
+    T c1 = (in && lt <= k1) ? x : (T)0, c2 = (in && lt <= k2) ? x : (T)0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const T d1 = __shfl_xor(c1, o), d2 = __shfl_xor(c2, o);
+        c1 = d1 > c1 ? d1 : c1;
+        c2 = d2 > c2 ? d2 : c2;
+    }
+    if (lane == 0) {
+        atomicMax(&s_sel[0], (unsigned long long)c1);
+        atomicMax(&s_sel[1], (unsigned long long)c2);
+    }
 }
 constexpr int kTailThreads = 512;
 constexpr int kTailWin = kTailThreads;  // one position per thread
@@ -1431,56 +1474,22 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
     double mean;
     if (n <= kTailWin) {  // (uniform)
         const bool in = t < n;
-        const unsigned long long x = in ? key(t) : ~0ull;  // (the pads never smaller than a key)
-        s_key[t] = x;
-        if (t < 2) s_sel[t] = 0ull;
-        unsigned long long v[1] = {x};
-        wave_bitonic<1>(v);  // each wave's keys sorted by shuffles
-        s_run[t] = v[0];
-        __syncthreads();
-        TAIL_STAMP(1);
-        // the keys smaller than x: x <= (k-th smallest) iff at most k keys are smaller, so the
-        // k-th smallest is the largest such x.  Counted by a branchless binary search in every
-        // wave's sorted run, the eight searches interleaved (an all-pairs compare loop cost 10k
-        // cycles of 64-bit VALU compares per window)
-        // (by the waves that hold keys, in the runs that hold keys: a guard per run inside one
-        // unrolled loop compiled to a branch and a wait per read)
-        const int nr = (int)((n + 63) / 64);
-        int lt = 0;
-        if (wave < nr) {
-            switch (nr) {  // (uniform; the search of nr runs unrolled at compile time)
-                case 1: lt = runs_below<1>(s_run, x); break;
-                case 2: lt = runs_below<2>(s_run, x); break;
-                case 3: lt = runs_below<3>(s_run, x); break;
-                case 4: lt = runs_below<4>(s_run, x); break;
-                case 5: lt = runs_below<5>(s_run, x); break;
-                case 6: lt = runs_below<6>(s_run, x); break;
-                case 7: lt = runs_below<7>(s_run, x); break;
-                default: lt = runs_below<8>(s_run, x); break;
-            }
-        }
-        // the largest candidate of each wave (shuffles), then one LDS max per wave (an atomicMax of
-        // every lane compiled to a scalar loop over the lanes, ~10 us per window)
-        unsigned long long c1 = (in && lt <= k1) ? x : 0ull, c2 = (in && lt <= k2) ? x : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long d1 = __shfl_xor(c1, o), d2 = __shfl_xor(c2, o);
-            c1 = d1 > c1 ? d1 : c1;
-            c2 = d2 > c2 ? d2 : c2;
-        }
-        if (lane == 0) {
-            atomicMax(&s_sel[0], c1);
-            atomicMax(&s_sel[1], c2);
-        }
-        TAIL_STAMP(2);
-        if (q == 0) {  // (uniform) the exact integer sum
-            long long cs = in ? (long long)x : 0;
-            cs = block_sum_i64(cs, s_red);  // (contains the barriers after the rank writes)
+        if (t < 2) s_sel[t] = 0ull;  // (read after window_kth's and the mean's barriers)
+        if (q == 0) {  // (uniform) coverage: 32-bit keys; the exact integer sum
+            const uint32_t x = in ? (uint32_t)cov[lo + t] : ~0u;
+            window_kth<uint32_t>(x, in, n, k1, k2, (uint32_t*)s_run, s_sel);
+            TAIL_STAMP(1);
+            const long long cs = block_sum_i64(in ? (long long)x : 0, s_red);  // (its barriers order s_sel)
             mean = (double)cs / (double)n;
-        } else {  // numpy's pairwise mean over the window (values in LDS, as doubles)
+        } else {  // the entropies' bit patterns; numpy's pairwise mean over the window in LDS
+            const unsigned long long x = in ? key(t) : ~0ull;
+            s_key[t] = x;
+            window_kth<unsigned long long>(x, in, n, k1, k2, s_run, s_sel);
+            TAIL_STAMP(1);
             __syncthreads();
             mean = pw_fast<kTailThreads, 4>((const double*)s_key, (int)n, s_val) / (double)n;  // (n <= 512)
         }
+        TAIL_STAMP(2);
         a = s_sel[0];
         b = s_sel[1];
         TAIL_STAMP(3);

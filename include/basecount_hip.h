@@ -42,7 +42,7 @@ extern "C" {
 #define BC_E_NODEV (-4) /* no usable gfx950 device                                               */
 #define BC_E_COMM (-5)  /* RCCL error in a multi-GPU call                                        */
 
-#define BC_ABI_VERSION 7
+#define BC_ABI_VERSION 8
 
 /* Layouts of bc_reads.seq.
  *   BC_SEQ_BAM   BAM packing: "=ACMGRSVTWYHKDBN" codes, two per byte, high nibble first

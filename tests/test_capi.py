@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(header, lib):
 def test_hip_library_reports_no_device_without_gpu():
     from basecount_amd import device as D
 
-    assert D.lib().bc_abi_version() == 7
+    assert D.lib().bc_abi_version() == 8
     # the shipped build has no work-skipping diagnostics compiled in
     assert D.build_info().startswith("gfx950") and "diag=0" in D.build_info()
     n = D.device_count()

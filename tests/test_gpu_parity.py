@@ -860,6 +860,10 @@ def test_pileup_summary_amplicons_fused_tail(ctx, L, n, mbq, k):
     want = [np.mean(ocov.astype(np.int64)), np.mean(oent), float(np.count_nonzero(ocov)), float(ocov.astype(np.int64).sum())]
     tiles = [(int(a), int(a + w)) for a, w in zip(rng.integers(-20, L, 60), rng.integers(-3, 420, 60))]
     tiles += [(0, 0), (L - 1, L + 10), (5, 4), (100, 100 + 1_500), (0, L - 1)]
+    # every count of sorted 64-key runs (n = 64, 65, 449, 512), the first radix-select size (513),
+    # and enough windows for more blocks than CUs (3 per window + the summary's)
+    tiles += [(7, 7 + 63), (7, 7 + 64), (3, 3 + 448), (11, 11 + 511), (2, 2 + 512)]
+    tiles += [(int(a), int(a + w)) for a, w in zip(rng.integers(0, L, 30), rng.integers(200, 280, 30))]
     lo = np.array([t[0] for t in tiles], np.int64)
     hi = np.array([t[1] for t in tiles], np.int64)
     ctx.set_shape("rc")

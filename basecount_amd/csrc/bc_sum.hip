@@ -118,18 +118,17 @@ __global__ __launch_bounds__(256) void k_sum_reads(PileArgs A) {
     }
 }
 
-// The counts of the lane's position in tile t (k_pileup_solo's walk of one tile, its reads found
-// by one search).
+// The counts of the lane's position in tile t (k_pileup_solo's walk of one tile) from its reads
+// [lo, hi) (lo < 0: found by one search here).
 template <bool QUAL, int K>
 __device__ __forceinline__ void tile_counts(const PileArgs& A, int64_t t, int lane, uint4* myrec, uint8_t* mystage,
-                                            bool qual_vec, uint32_t (&cnt)[6]) {
+                                            bool qual_vec, uint32_t (&cnt)[6], int64_t lo = -1, int64_t hi = -1) {
     const int64_t t0 = t * kTile, P = t0 + lane, L = A.L;
     const int gb = (int)t0 + 8 * (lane >> 3);
     const int s8 = lane & 7;
 #pragma unroll
     for (int c = 0; c < 6; ++c) cnt[c] = 0;
-    int64_t lo, hi;
-    lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
+    if (lo < 0) lower_bound_pair(A.pos, A.n, t0 - A.max_span + 1, t0 + kTile, lane, lo, hi);
     if (hi <= lo) return;
     int64_t bad = INT64_MAX;
     const bool edge = t0 + kTile > L;
@@ -195,10 +194,15 @@ __global__ __launch_bounds__(256, 2) void k_sum_exact(PileArgs A) {
         const int64_t s = it - A.n_tail_tiles;
         const int64_t l = A.dlist[s];
         uint32_t cov0, cov1;
-        tile_counts<QUAL, K>(A, 2 * l, lane, myrec, mystage, qual_vec, cnt);
+        // both tiles' read ranges in one search (a quarter-wave per bound), not one search per tile
+        const int64_t t0 = 2 * l * kTile;
+        const int64_t keys[4] = {t0 - A.max_span + 1, t0 + kTile, t0 + kTile - A.max_span + 1, t0 + 2 * kTile};
+        int64_t rg[4];
+        lower_bound_quad(A.pos, A.n, keys, lane, rg);
+        tile_counts<QUAL, K>(A, 2 * l, lane, myrec, mystage, qual_vec, cnt, rg[0], rg[1]);
         const double h0 = position_entropy<K>(cnt, A.nf, cov0);
         const double half = leaf_half(h0, lane, tr);
-        tile_counts<QUAL, K>(A, 2 * l + 1, lane, myrec, mystage, qual_vec, cnt);
+        tile_counts<QUAL, K>(A, 2 * l + 1, lane, myrec, mystage, qual_vec, cnt, rg[2], rg[3]);
         const double h1 = position_entropy<K>(cnt, A.nf, cov1);
         const double leaf = leaf_finish(half, h1, lane, tr);
         const long long cs = wave_sum_i64((long long)cov0 + cov1);

@@ -158,6 +158,47 @@ __device__ __forceinline__ void lower_bound_pair(const int32_t* pos, int64_t n, 
         lower_bound_pair_t<int64_t>(pos, n, v_lo, v_hi, lane, r_lo, r_hi);
 }
 
+// Four lower bounds searched together, a quarter-wave (16 lanes, 16 probes per round) per key:
+// about as many rounds as lower_bound_pair's two (17-ary instead of 33-ary), for two tiles' ranges
+// at once.  r[q] = lower_bound(v[q]), wave-uniform.
+template <typename IT>
+__device__ __forceinline__ void lower_bound_quad_t(const int32_t* pos, IT n, const int64_t (&v)[4], int lane,
+                                                   int64_t (&r)[4]) {
+    const int h = lane >> 4, l = lane & 15;
+    const int64_t key = h == 0 ? v[0] : h == 1 ? v[1] : h == 2 ? v[2] : v[3];
+    IT lo = 0, hi = n;  // answer in [lo, hi] (per quarter)
+    while (__any(hi - lo > 16)) {
+        const bool act = hi - lo > 16;
+        const IT s = act ? ((hi - lo) / 17 > 0 ? (hi - lo) / 17 : 1) : 1;
+        const IT idx = lo + (IT)(l + 1) * s;
+        const bool less = act && idx < hi && (int64_t)pos[idx] < key;
+        const unsigned long long m = __ballot(less);
+        const IT c = (IT)__popc((unsigned)(m >> (16 * h)) & 0xFFFFu);
+        if (act) {
+            const IT nlo = c ? lo + c * s + 1 : lo;
+            const IT nhi = (c < 16 && lo + (c + 1) * s < hi) ? lo + (c + 1) * s : hi;
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    const IT idx = lo + (IT)l;
+    const bool less = idx < hi && (int64_t)pos[idx] < key;
+    const unsigned long long m = __ballot(less);
+    const int64_t res = (int64_t)lo + __popc((unsigned)(m >> (16 * h)) & 0xFFFFu);
+    const uint32_t rl = (uint32_t)res, rh = (uint32_t)((uint64_t)res >> 32);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        r[q] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rh, 16 * q) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)rl, 16 * q));
+}
+__device__ __forceinline__ void lower_bound_quad(const int32_t* pos, int64_t n, const int64_t (&v)[4], int lane,
+                                                 int64_t (&r)[4]) {
+    if (n < (int64_t)0x7FFFFFC0)
+        lower_bound_quad_t<uint32_t>(pos, (uint32_t)n, v, lane, r);
+    else
+        lower_bound_quad_t<int64_t>(pos, n, v, lane, r);
+}
+
 __device__ __forceinline__ void flush_acc(unsigned long long& acc, uint32_t (&cnt)[6]) {
 #pragma unroll
     for (int c = 0; c < 6; ++c) cnt[c] += (uint32_t)(acc >> (kField * c)) & ((1u << kField) - 1);

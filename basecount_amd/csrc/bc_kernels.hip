@@ -1311,7 +1311,7 @@ __global__ __launch_bounds__(256) void k_amplicon(const int32_t* cov, const doub
 // every buffer's 64 partials (k_stats_lane<LEAVES>: a whole buffer's 128-position leaves, the
 // partial buffer's nodes one level above its leaves) added up numpy's tree by a wave, the
 // buffers folded in order, the exact coverage sum and non-zero count.  The windows' medians: a
-// window of <= 512 positions is loaded one element per thread, each wave sorts its 64 keys
+// window of <= 320 positions (kTailWin) is loaded one element per thread, each wave sorts its 64 keys
 // (shuffles), and each thread counts the keys smaller than its own by a binary search in every
 // wave's sorted run: the k-th smallest value is the largest one with at most k smaller keys (a
 // wave max, then an LDS atomic max); longer windows take the radix select.  The means: numpy's
@@ -1347,7 +1347,7 @@ __device__ __forceinline__ int runs_below(const T* run, T x) {
 // lane compiled to a scalar loop over the lanes, ~10 us per window) into s_sel (zeroed, read
 // after the caller's next barrier).  T: the coverage's 32 bits (half the shuffles and compares)
 // or an entropy's 64.  An all-pairs compare loop cost 10k cycles per window.
-template <typename T>
+template <typename T, int NWM>
 __device__ __forceinline__ void window_kth(T x, bool in, int64_t n, int64_t k1, int64_t k2, T* s_run,
                                            unsigned long long* s_sel) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1358,15 +1358,14 @@ __device__ __forceinline__ void window_kth(T x, bool in, int64_t n, int64_t k1, 
     const int nr = (int)((n + 63) / 64);
     int lt = 0;
     if (wave < nr) {
-        switch (nr) {  // (uniform; the search of nr runs unrolled at compile time)
+        // (uniform; the search of nr runs unrolled at compile time; nr <= NWM, and the runs
+        // past n hold pads only, which count 0)
+        switch (nr) {
             case 1: lt = runs_below<1, T>(s_run, x); break;
             case 2: lt = runs_below<2, T>(s_run, x); break;
             case 3: lt = runs_below<3, T>(s_run, x); break;
             case 4: lt = runs_below<4, T>(s_run, x); break;
-            case 5: lt = runs_below<5, T>(s_run, x); break;
-            case 6: lt = runs_below<6, T>(s_run, x); break;
-            case 7: lt = runs_below<7, T>(s_run, x); break;
-            default: lt = runs_below<8, T>(s_run, x); break;
+            default: lt = runs_below<NWM, T>(s_run, x); break;
         }
     }
     T c1 = (in && lt <= k1) ? x : (T)0, c2 = (in && lt <= k2) ? x : (T)0;
@@ -1381,7 +1380,7 @@ __device__ __forceinline__ void window_kth(T x, bool in, int64_t n, int64_t k1, 
         atomicMax(&s_sel[1], (unsigned long long)c2);
     }
 }
-constexpr int kTailThreads = 512;
+constexpr int kTailThreads = 320;  // five waves: amplicon windows (C4: 201-279 positions) in one pass
 constexpr int kTailWin = kTailThreads;  // one position per thread
 __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const double* ent, const double* sec, int64_t L,
                                               const int64_t* lo_a, const int64_t* hi_a, int n_tiles, double* amp,
@@ -1477,17 +1476,17 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(const int32_t* cov, const
         if (t < 2) s_sel[t] = 0ull;  // (read after window_kth's and the mean's barriers)
         if (q == 0) {  // (uniform) coverage: 32-bit keys; the exact integer sum
             const uint32_t x = in ? (uint32_t)cov[lo + t] : ~0u;
-            window_kth<uint32_t>(x, in, n, k1, k2, (uint32_t*)s_run, s_sel);
+            window_kth<uint32_t, NW>(x, in, n, k1, k2, (uint32_t*)s_run, s_sel);
             TAIL_STAMP(1);
             const long long cs = block_sum_i64(in ? (long long)x : 0, s_red);  // (its barriers order s_sel)
             mean = (double)cs / (double)n;
         } else {  // the entropies' bit patterns; numpy's pairwise mean over the window in LDS
             const unsigned long long x = in ? key(t) : ~0ull;
             s_key[t] = x;
-            window_kth<unsigned long long>(x, in, n, k1, k2, s_run, s_sel);
+            window_kth<unsigned long long, NW>(x, in, n, k1, k2, s_run, s_sel);
             TAIL_STAMP(1);
             __syncthreads();
-            mean = pw_fast<kTailThreads, 4>((const double*)s_key, (int)n, s_val) / (double)n;  // (n <= 512)
+            mean = pw_fast<kTailThreads, 4>((const double*)s_key, (int)n, s_val) / (double)n;  // (n <= kTailWin)
         }
         TAIL_STAMP(2);
         a = s_sel[0];

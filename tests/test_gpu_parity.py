@@ -844,7 +844,10 @@ def test_amplicons_match_numpy(ctx, wmax, ties):
 
 
 @pytest.mark.parametrize("L,n,mbq,k", [(8192 * 3 + 1711, 60_000, 0, 5), (8192 * 2, 40_000, 20, 6),
-                                        (5_000, 30_000, 0, 5), (40_003, 50_000, 0, 6)])
+                                        (5_000, 30_000, 0, 5), (40_003, 50_000, 0, 6),
+                                        # the partial buffer's tree: below numpy's 8-element rule,
+                                        # one split past a 128-leaf, a reference shorter than a leaf
+                                        (8192 + 5, 20_000, 0, 5), (8192 + 130, 20_000, 0, 6), (100, 2_000, 0, 5)])
 def test_pileup_summary_amplicons_fused_tail(ctx, L, n, mbq, k):
     """bc_pileup_summary_amplicons on the read-chunked path (kernel 1, kernel 2 with numpy's leaf
     partials, then ONE launch for the summary fold and every window): the summary's four numbers
